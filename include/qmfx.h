@@ -1,0 +1,125 @@
+/*
+ * qmfx.h: C ABI of the MI355X (gfx950) implicit-feedback MF engine.
+ *
+ * This is the device layer under the drop-in qmf::Engine API (qmf_amd/host/qmf/).  It
+ * replaces the reference's in-process CPU hot path (taozhijiang/qmf, paths relative to the
+ * reference root):
+ *
+ *   qmf/wals/WALSEngine.cpp:165-218  WALSEngine::iterate           -> qmfx_wals_half
+ *   qmf/wals/WALSEngine.cpp:246-264  WALSEngine::computeXtX        -> inside qmfx_wals_half
+ *   qmf/wals/WALSEngine.cpp:266-310  WALSEngine::updateFactorsForOne -> inside qmfx_wals_half
+ *   qmf/Matrix.cpp:81-96             linearSymmetricSolve (dsysv_) -> inside qmfx_wals_half
+ *   qmf/wals/WALSEngine.cpp:130-163  groupSignals (CSR build)      -> qmfx_upload_csr / qmfx_gen_synthetic
+ *   qmf/FactorData.h:55-100          FactorData::setFactors        -> qmfx_set_factors / qmfx_fill_uniform
+ *   qmf/bpr/BPREngine.cpp:146-220    BPREngine::optimize / update  -> qmfx_bpr_epoch / qmfx_bpr_apply
+ *   qmf/bpr/BPREngine.cpp:246-274    BPREngine::evaluate (loss)    -> qmfx_bpr_eval
+ *   distributed/ (TCP broadcast + bucket gather)                   -> qmfx_dist_init + qmfx_wals_half
+ *                                                                     (RCCL all-gather over xGMI)
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types.  Host buffers are copied;
+ * device buffers are owned by the context.  Every call returns 0 on success or a negative
+ * code, with a message from qmfx_last_error() (thread-local).  The reference aborts on
+ * errors (glog CHECK); the C++ wrapper converts a non-zero status into that abort.  One
+ * caller thread per context.  Sides: 0 = users, 1 = items.  Factors cross the ABI as
+ * row-major float64 n×k (the reference's Double = double, qmf/Types.h:24); on the device
+ * they are stored in the context precision (32 or 64) with rows padded to a multiple of 16.
+ */
+#ifndef QMFX_H_
+#define QMFX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qmfx_ctx qmfx_ctx;
+
+#define QMFX_USERS 0
+#define QMFX_ITEMS 1
+
+/* ---- library / context ---------------------------------------------------------------- */
+const char* qmfx_last_error(void);
+int qmfx_version(void);
+int qmfx_device_count(int* count);
+
+/* precision: 32 or 64.  nfactors: the reference's --nfactors (WALSConfig/BPRConfig). */
+int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors);
+int qmfx_destroy(qmfx_ctx* ctx);
+int qmfx_sync(qmfx_ctx* ctx);
+int qmfx_set_shape(qmfx_ctx* ctx, int64_t nusers, int64_t nitems);
+int qmfx_get_shape(qmfx_ctx* ctx, int64_t* nusers, int64_t* nitems, int64_t* nnz);
+
+/* ---- interactions (WALSEngine.cpp:130-163) --------------------------------------------- */
+/* CSR of `side`: rowptr[n_side+1], colidx[nnz] = row index on the other side, values[nnz]. */
+int qmfx_upload_csr(qmfx_ctx* ctx, int side, const int64_t* rowptr, const int32_t* colidx,
+                    const double* values, int64_t nnz);
+/* Device-generated synthetic matrix: ~nnz uniform unique (u, i) pairs,
+ * w in 1..5, both orientations built on the device.  *nnz_out = unique pairs kept. */
+int qmfx_gen_synthetic(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t nnz,
+                       uint64_t seed, int64_t* nnz_out);
+/* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data). */
+int qmfx_download_csr(qmfx_ctx* ctx, int side, int64_t* rowptr, int32_t* colidx,
+                      float* values);
+
+/* ---- factors (FactorData.h) ------------------------------------------------------------- */
+int qmfx_set_factors(qmfx_ctx* ctx, int side, const double* rowmajor);
+int qmfx_get_factors(qmfx_ctx* ctx, int side, double* rowmajor);
+int qmfx_fill_uniform(qmfx_ctx* ctx, int side, double bound, uint64_t seed);
+
+/* ---- WALS (WALSEngine.cpp:165-218) -------------------------------------------------------
+ * Solves every row of `side` with the other side fixed: X ← 0, G = YᵀY, per row
+ * A = G + Σ αv yyᵀ + λI, b = Σ (1+αv) y, x = A⁻¹b.  *loss_sum receives Σ over solved rows of
+ * Σ(1+αv) + xᵀ(A−λI)x − 2xᵀb (divide by nusers·nitems for the reference's printed loss).
+ * With a distributed context the local row range is solved and the factor matrix is
+ * all-gathered over RCCL before returning; the loss is then the global sum. */
+int qmfx_wals_half(qmfx_ctx* ctx, int side, double alpha, double lambda, double* loss_sum);
+/* Number of rows whose system was not positive definite in the last half (a non-positive
+ * Cholesky pivot: only possible when some 1 + α·v < 0 or λ ≤ 0).  Their indices are
+ * written to rows[] (up to cap).  The C++ engine re-solves them on the host with an LDLᵀ
+ * (Bunch-Kaufman) solve, as dsysv_ would. */
+int qmfx_wals_failed_rows(qmfx_ctx* ctx, int64_t* rows, int64_t cap, int64_t* count);
+/* Host-side re-solve input for a failed row: A (k×k row-major, λ included) and b. */
+int qmfx_wals_row_system(qmfx_ctx* ctx, int side, int64_t row, double alpha, double lambda,
+                         double* A, double* b, double* csum);
+int qmfx_wals_set_row(qmfx_ctx* ctx, int side, int64_t row, const double* x);
+
+/* ---- BPR (BPREngine.cpp:146-274) ---------------------------------------------------------
+ * Positives in data order as (user idx, item idx) (BPREngine::init :65-82).  Builds the
+ * per-user sorted positive lists used for negative rejection. */
+int qmfx_bpr_set_positives(qmfx_ctx* ctx, const int64_t* users, const int64_t* items,
+                           int64_t npos);
+int qmfx_bpr_set_biases(qmfx_ctx* ctx, const double* bias);  /* nitems values */
+int qmfx_bpr_get_biases(qmfx_ctx* ctx, double* bias);
+/* One Hogwild epoch over all positives × num_neg sampled negatives, visiting positives in
+ * a seed-dependent permuted order when shuffle != 0. */
+int qmfx_bpr_epoch(qmfx_ctx* ctx, uint64_t seed, int num_neg, double lr, double bias_lambda,
+                   double user_lambda, double item_lambda, int use_biases, int shuffle);
+/* Applies the given (u, p, n) triplets in order with one wave (exact update order). */
+int qmfx_bpr_apply(qmfx_ctx* ctx, const int64_t* triplets, int64_t n, double lr,
+                   double bias_lambda, double user_lambda, double item_lambda, int use_biases);
+/* Σ log(1+exp(−x̂)) over triplets (host array, uploaded and cached per `slot` 0/1). */
+int qmfx_bpr_eval(qmfx_ctx* ctx, int slot, const int64_t* triplets, int64_t n, int use_biases,
+                  double* loss_sum);
+
+/* ---- multi-GPU (one process per GPU; RCCL over xGMI) -------------------------------------- */
+int qmfx_rccl_unique_id(uint8_t* id128);
+int qmfx_dist_init(qmfx_ctx* ctx, int rank, int world, const uint8_t* id128);
+/* nnz-balanced contiguous row range owned by `rank` (host-only helper, no GPU needed). */
+int qmfx_partition_rows(const int64_t* rowptr, int64_t nrows, int world, int rank,
+                        int64_t* begin, int64_t* end);
+
+/* ---- measurement -------------------------------------------------------------------------- */
+/* HIP-event time of the row-solve kernel launches (on the context stream) since reset. */
+int qmfx_solve_kernel_stats(qmfx_ctx* ctx, double* total_ms, int64_t* launches,
+                            double* flops, double* bytes);
+int qmfx_reset_stats(qmfx_ctx* ctx);
+
+/* ---- self tests ------------------------------------------------------------------------------ */
+/* C(16×16) = A(16×4)·B(4×16) through the kernels' MFMA operand/accumulator maps. */
+int qmfx_selftest_mfma(int device, int precision, const double* A, const double* B, double* C);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QMFX_H_ */

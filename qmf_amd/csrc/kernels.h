@@ -1,0 +1,90 @@
+// Kernel argument structs and host launchers shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qmfx {
+
+template <typename T>
+struct SolveArgs {
+  const int64_t* rowptr;  // CSR of the side being solved
+  const int32_t* col;     // column = row index on the fixed side
+  const T* val;           // raw interaction value v
+  const T* Y;             // fixed-side factors [nY][KP]
+  const T* G;             // YᵀY, KP×KP
+  T* X;                   // solved-side factors [nX][KP]
+  double* rowloss;        // [nX]
+  int32_t* status;        // [nX] non-zero: non-positive pivot (system not SPD)
+  const int64_t* order;   // optional processing order (nullptr = identity)
+  int64_t row_begin;      // first slot of the order handled by this launch
+  int64_t nrows;          // number of rows (blocks)
+  T alpha;
+  T lambda;
+  int k;                  // real number of factors (≤ KP)
+};
+
+hipError_t launch_wals_solve_f32(const SolveArgs<float>& a, int nt, hipStream_t s);
+hipError_t launch_wals_solve_f64(const SolveArgs<double>& a, int nt, hipStream_t s);
+hipError_t launch_gram_f32(const float* Y, int64_t n, int nt, float* G, double* partial,
+                           int max_blocks, hipStream_t s);
+hipError_t launch_gram_f64(const double* Y, int64_t n, int nt, double* G, double* partial,
+                           int max_blocks, hipStream_t s);
+hipError_t launch_sum_f64(const double* x, int64_t n, double* out, hipStream_t s);
+hipError_t launch_mfma_selftest_f32(const float* A, const float* B, float* C, hipStream_t s);
+hipError_t launch_mfma_selftest_f64(const double* A, const double* B, double* C,
+                                    hipStream_t s);
+
+// BPR (bpr.hip)
+template <typename T>
+struct BprArgs {
+  T* U;                    // [nu][KP]
+  T* I;                    // [ni][KP]
+  T* bias;                 // [ni] or nullptr
+  const int64_t* pos_user; // positives in data order
+  const int32_t* pos_item;
+  int64_t npos;
+  const int64_t* urowptr;  // user -> sorted positive items (rejection set)
+  const int32_t* uitems;
+  int64_t nitems;
+  int num_neg;
+  uint64_t seed;
+  uint64_t perm_a, perm_b; // epoch permutation of positives: idx = (a*i + b) mod npos
+  T lr, bias_lambda, user_lambda, item_lambda;
+  int use_biases;
+  int kp;                  // row stride (padded factors)
+  int32_t* bad;            // set to 1 if a derivative was not finite
+};
+
+hipError_t launch_bpr_epoch_f32(const BprArgs<float>& a, int kp, hipStream_t s);
+hipError_t launch_bpr_epoch_f64(const BprArgs<double>& a, int kp, hipStream_t s);
+hipError_t launch_bpr_apply_f32(const BprArgs<float>& a, const int64_t* trip, int64_t n,
+                                int kp, hipStream_t s);
+hipError_t launch_bpr_apply_f64(const BprArgs<double>& a, const int64_t* trip, int64_t n,
+                                int kp, hipStream_t s);
+hipError_t launch_bpr_eval_f32(const float* U, const float* I, const float* bias,
+                               const int64_t* trip, int64_t n, int kp, int use_biases,
+                               double* partial, double* out, hipStream_t s);
+hipError_t launch_bpr_eval_f64(const double* U, const double* I, const double* bias,
+                               const int64_t* trip, int64_t n, int kp, int use_biases,
+                               double* partial, double* out, hipStream_t s);
+
+// Synthetic data + CSR build (data.hip)
+hipError_t launch_synth_keys(uint64_t* keys, int64_t n, uint64_t space, uint64_t seed,
+                             hipStream_t s);
+hipError_t build_csr_from_sorted_keys(const uint64_t* keys, int64_t nnz, int64_t nrows,
+                                      uint64_t ncols, int64_t* rowptr, int32_t* col,
+                                      hipStream_t s);
+hipError_t launch_transpose_keys(const uint64_t* keys, int64_t nnz, uint64_t ncols,
+                                 uint64_t nrows, uint64_t* out, hipStream_t s);
+hipError_t launch_synth_values_any(const uint64_t* keys, int64_t n, uint64_t div,
+                                   uint64_t nitems, int user_major, uint64_t seed, void* val,
+                                   int prec, hipStream_t s);
+hipError_t sort_unique_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int64_t* n_out,
+                            int end_bit, hipStream_t s);
+hipError_t sort_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int end_bit, hipStream_t s);
+hipError_t launch_fill_uniform_f32(float* X, int64_t n, int kp, int k, double bound,
+                                   uint64_t seed, hipStream_t s);
+hipError_t launch_fill_uniform_f64(double* X, int64_t n, int kp, int k, double bound,
+                                   uint64_t seed, hipStream_t s);
+
+}  // namespace qmfx

@@ -1,0 +1,879 @@
+// Host side of the qmfx C ABI (include/qmfx.h): context, device buffers, orchestration of
+// the WALS half-epoch and BPR epoch kernels, RCCL data path for multi-GPU.
+#include "../../include/qmfx.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+using namespace qmfx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m, int code = -1) {
+  g_err = m;
+  return code;
+}
+
+#define HIPCHK(x)                                                                     \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_), -2); \
+  } while (0)
+
+#define NCCLCHK(x)                                                                      \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) return fail(std::string(#x) + ": " + ncclGetErrorString(r_), -3); \
+  } while (0)
+
+struct SideBuf {
+  int64_t n = 0;
+  int64_t nnz = 0;
+  int64_t* rowptr = nullptr;
+  int32_t* col = nullptr;
+  void* val = nullptr;
+  void* F = nullptr;
+  std::vector<int64_t> h_rowptr;
+  int64_t rbeg = 0, rend = 0;           // rows solved by this rank
+  std::vector<int64_t> bounds;          // per-rank row boundaries (world+1)
+};
+
+}  // namespace
+
+struct qmfx_ctx {
+  int device = 0;
+  int prec = 32;
+  int k = 0, kp = 0, nt = 0;
+  size_t esz = 4;
+  hipStream_t stream = nullptr;
+  SideBuf s[2];
+  int64_t nnz = 0;
+  void* G = nullptr;
+  double* gpart = nullptr;
+  int gpart_blocks = 1024;
+  double* rowloss = nullptr;
+  int64_t rowloss_cap = 0;
+  int32_t* status = nullptr;
+  double* dsum = nullptr;
+  double* hsum = nullptr;  // pinned
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double solve_ms = 0, solve_flops = 0, solve_bytes = 0;
+  int64_t solve_launches = 0;
+  int last_side = 0;
+  // distributed
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+  // BPR
+  int64_t* pos_user = nullptr;
+  int32_t* pos_item = nullptr;
+  int64_t npos = 0;
+  int64_t* urowptr = nullptr;
+  int32_t* uitems = nullptr;
+  void* bias = nullptr;
+  int32_t* bad = nullptr;
+  int64_t* trip[2] = {nullptr, nullptr};
+  int64_t trip_n[2] = {0, 0};
+  const void* trip_src[2] = {nullptr, nullptr};
+  double* eval_partial = nullptr;
+  uint64_t bpr_epochs = 0;
+};
+
+namespace {
+
+int set_dev(qmfx_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return 0;
+}
+
+void dfree(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <typename P>
+void dfree_t(P*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+int ensure_side_factors(qmfx_ctx* c, int side) {
+  SideBuf& sb = c->s[side];
+  if (sb.F) return 0;
+  if (sb.n <= 0) return fail("shape not set (qmfx_set_shape)");
+  HIPCHK(hipMalloc(&sb.F, (size_t)sb.n * c->kp * c->esz));
+  HIPCHK(hipMemsetAsync(sb.F, 0, (size_t)sb.n * c->kp * c->esz, c->stream));
+  return 0;
+}
+
+void set_default_bounds(SideBuf& sb, int world, int rank) {
+  sb.bounds.assign(world + 1, 0);
+  const int64_t total = sb.h_rowptr.empty() ? 0 : sb.h_rowptr.back();
+  for (int r = 0; r <= world; ++r) {
+    if (r == world) {
+      sb.bounds[r] = sb.n;
+    } else if (r == 0) {
+      sb.bounds[r] = 0;
+    } else {
+      const int64_t target = (int64_t)((__int128)total * r / world);
+      sb.bounds[r] = std::lower_bound(sb.h_rowptr.begin(), sb.h_rowptr.end(), target) -
+                     sb.h_rowptr.begin();
+      if (sb.bounds[r] > sb.n) sb.bounds[r] = sb.n;
+    }
+  }
+  for (int r = 1; r <= world; ++r) sb.bounds[r] = std::max(sb.bounds[r], sb.bounds[r - 1]);
+  sb.rbeg = sb.bounds[rank];
+  sb.rend = sb.bounds[rank + 1];
+}
+
+int ensure_rowloss(qmfx_ctx* c, int64_t n) {
+  if (c->rowloss_cap >= n) return 0;
+  dfree_t(c->rowloss);
+  dfree_t(c->status);
+  HIPCHK(hipMalloc(&c->rowloss, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+  HIPCHK(hipMalloc(&c->status, (size_t)std::max<int64_t>(n, 1) * sizeof(int32_t)));
+  c->rowloss_cap = n;
+  return 0;
+}
+
+template <typename T>
+std::vector<T> convert(const double* src, size_t n) {
+  std::vector<T> v(n);
+  for (size_t i = 0; i < n; ++i) v[i] = (T)src[i];
+  return v;
+}
+
+ncclDataType_t nccl_type(int prec) { return prec == 32 ? ncclFloat32 : ncclFloat64; }
+
+// Every transfer goes through the context's (non-blocking) stream so it is ordered with the
+// kernels and async memsets issued there; the call returns when the copy has completed.
+hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  if (bytes == 0) return hipSuccess;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->stream);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(c->stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* qmfx_last_error(void) { return g_err.c_str(); }
+int qmfx_version(void) { return 1; }
+
+int qmfx_device_count(int* count) {
+  HIPCHK(hipGetDeviceCount(count));
+  return 0;
+}
+
+int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
+  if (!out) return fail("out is null");
+  if (precision != 32 && precision != 64) return fail("precision must be 32 or 64");
+  if (nfactors <= 0) return fail("nfactors must be positive");
+  const int nt = (nfactors + 15) / 16;
+  if (precision == 32 && nt > 8) return fail("nfactors > 128 not supported in fp32 yet");
+  if (precision == 64 && nt > 4) return fail("nfactors > 64 not supported in fp64 yet");
+  auto* c = new qmfx_ctx();
+  c->device = device;
+  c->prec = precision;
+  c->k = nfactors;
+  c->nt = nt;
+  c->kp = 16 * nt;
+  c->esz = precision == 32 ? 4 : 8;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->G, (size_t)c->kp * c->kp * c->esz);
+  if (e == hipSuccess)
+    e = hipMalloc(&c->gpart, (size_t)c->gpart_blocks * (nt * (nt + 1) / 2) * 256 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->dsum, 4 * sizeof(double));
+  if (e == hipSuccess) e = hipHostMalloc(&c->hsum, 4 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->bad, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&c->eval_partial, 1024 * sizeof(double));
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e != hipSuccess) {
+    g_err = std::string("qmfx_create: ") + hipGetErrorString(e);
+    delete c;
+    return -2;
+  }
+  *out = c;
+  return 0;
+}
+
+int qmfx_destroy(qmfx_ctx* c) {
+  if (!c) return 0;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (auto& sb : c->s) {
+    dfree_t(sb.rowptr);
+    dfree_t(sb.col);
+    dfree(sb.val);
+    dfree(sb.F);
+  }
+  dfree(c->G);
+  dfree_t(c->gpart);
+  dfree_t(c->rowloss);
+  dfree_t(c->status);
+  dfree_t(c->dsum);
+  if (c->hsum) hipHostFree(c->hsum);
+  dfree_t(c->bad);
+  dfree_t(c->eval_partial);
+  dfree_t(c->pos_user);
+  dfree_t(c->pos_item);
+  dfree_t(c->urowptr);
+  dfree_t(c->uitems);
+  dfree(c->bias);
+  dfree_t(c->trip[0]);
+  dfree_t(c->trip[1]);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int qmfx_sync(qmfx_ctx* c) {
+  if (set_dev(c)) return -2;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int qmfx_set_shape(qmfx_ctx* c, int64_t nusers, int64_t nitems) {
+  if (nusers <= 0 || nitems <= 0) return fail("empty shape: nusers and nitems must be > 0");
+  if (nitems > 0x7fffffffll || nusers > 0x7fffffffll) return fail("more than 2^31 rows");
+  if (set_dev(c)) return -2;
+  for (int side = 0; side < 2; ++side) {
+    const int64_t n = side == 0 ? nusers : nitems;
+    if (c->s[side].n != n) {
+      dfree(c->s[side].F);
+      dfree_t(c->s[side].rowptr);
+      dfree_t(c->s[side].col);
+      dfree(c->s[side].val);
+      c->s[side].h_rowptr.clear();
+      c->s[side].n = n;
+    }
+  }
+  return 0;
+}
+
+int qmfx_get_shape(qmfx_ctx* c, int64_t* nusers, int64_t* nitems, int64_t* nnz) {
+  if (nusers) *nusers = c->s[0].n;
+  if (nitems) *nitems = c->s[1].n;
+  if (nnz) *nnz = c->nnz;
+  return 0;
+}
+
+int qmfx_upload_csr(qmfx_ctx* c, int side, const int64_t* rowptr, const int32_t* colidx,
+                    const double* values, int64_t nnz) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  SideBuf& sb = c->s[side];
+  if (sb.n <= 0) return fail("shape not set (qmfx_set_shape)");
+  const int64_t nother = c->s[1 - side].n;
+  if (rowptr[0] != 0 || rowptr[sb.n] != nnz) return fail("rowptr inconsistent with nnz");
+  for (int64_t r = 0; r < sb.n; ++r)
+    if (rowptr[r + 1] < rowptr[r]) return fail("rowptr not monotone");
+  for (int64_t e = 0; e < nnz; ++e)
+    if (colidx[e] < 0 || colidx[e] >= nother) return fail("column index out of range");
+  if (set_dev(c)) return -2;
+  dfree_t(sb.rowptr);
+  dfree_t(sb.col);
+  dfree(sb.val);
+  HIPCHK(hipMalloc(&sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t)));
+  HIPCHK(hipMalloc(&sb.col, (size_t)std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&sb.val, (size_t)std::max<int64_t>(nnz, 1) * c->esz));
+  HIPCHK(scopy(c, sb.rowptr, rowptr, (size_t)(sb.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nnz > 0) {
+    HIPCHK(scopy(c, sb.col, colidx, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (c->prec == 32) {
+      auto v = convert<float>(values, (size_t)nnz);
+      HIPCHK(scopy(c, sb.val, v.data(), (size_t)nnz * 4, hipMemcpyHostToDevice));
+    } else {
+      HIPCHK(scopy(c, sb.val, values, (size_t)nnz * 8, hipMemcpyHostToDevice));
+    }
+  }
+  sb.nnz = nnz;
+  c->nnz = nnz;
+  sb.h_rowptr.assign(rowptr, rowptr + sb.n + 1);
+  set_default_bounds(sb, c->world, c->rank);
+  return 0;
+}
+
+int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, float* values) {
+  SideBuf& sb = c->s[side];
+  if (!sb.rowptr) return fail("no CSR for this side");
+  if (set_dev(c)) return -2;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(scopy(c, rowptr, sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (sb.nnz > 0) {
+    HIPCHK(scopy(c, colidx, sb.col, (size_t)sb.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (c->prec == 32) {
+      HIPCHK(scopy(c, values, sb.val, (size_t)sb.nnz * 4, hipMemcpyDeviceToHost));
+    } else {
+      std::vector<double> v((size_t)sb.nnz);
+      HIPCHK(scopy(c, v.data(), sb.val, (size_t)sb.nnz * 8, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < v.size(); ++i) values[i] = (float)v[i];
+    }
+  }
+  return 0;
+}
+
+int qmfx_gen_synthetic(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz, uint64_t seed,
+                       int64_t* nnz_out) {
+  if (nnz <= 0) return fail("nnz must be positive");
+  if (int rc = qmfx_set_shape(c, nusers, nitems)) return rc;
+  const uint64_t space = (uint64_t)nusers * (uint64_t)nitems;
+  if ((uint64_t)nnz > space / 2) return fail("nnz too large for the shape");
+  int end_bit = 64 - __builtin_clzll(space);
+  uint64_t *keys = nullptr, *scratch = nullptr;
+  HIPCHK(hipMalloc(&keys, (size_t)nnz * 8));
+  HIPCHK(hipMalloc(&scratch, (size_t)nnz * 8));
+  HIPCHK(launch_synth_keys(keys, nnz, space, seed, c->stream));
+  int64_t m = 0;
+  HIPCHK(sort_unique_keys(keys, scratch, nnz, &m, end_bit, c->stream));
+  for (int side = 0; side < 2; ++side) {
+    SideBuf& sb = c->s[side];
+    dfree_t(sb.rowptr);
+    dfree_t(sb.col);
+    dfree(sb.val);
+    HIPCHK(hipMalloc(&sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t)));
+    HIPCHK(hipMalloc(&sb.col, (size_t)m * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&sb.val, (size_t)m * c->esz));
+    sb.nnz = m;
+  }
+  // users: keys are u·nitems + i, sorted
+  HIPCHK(build_csr_from_sorted_keys(keys, m, nusers, (uint64_t)nitems, c->s[0].rowptr,
+                                    c->s[0].col, c->stream));
+  HIPCHK(launch_synth_values_any(keys, m, (uint64_t)nitems, (uint64_t)nitems, 1, seed * 31 + 7,
+                                 c->s[0].val, c->prec, c->stream));
+  // items: transposed keys i·nusers + u, sorted
+  HIPCHK(launch_transpose_keys(keys, m, (uint64_t)nitems, (uint64_t)nusers, scratch, c->stream));
+  HIPCHK(sort_keys(scratch, keys, m, end_bit, c->stream));
+  HIPCHK(build_csr_from_sorted_keys(scratch, m, nitems, (uint64_t)nusers, c->s[1].rowptr,
+                                    c->s[1].col, c->stream));
+  HIPCHK(launch_synth_values_any(scratch, m, (uint64_t)nusers, (uint64_t)nitems, 0, seed * 31 + 7,
+                                 c->s[1].val, c->prec, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  hipFree(keys);
+  hipFree(scratch);
+  for (int side = 0; side < 2; ++side) {
+    SideBuf& sb = c->s[side];
+    sb.h_rowptr.resize(sb.n + 1);
+    HIPCHK(scopy(c, sb.h_rowptr.data(), sb.rowptr, (size_t)(sb.n + 1) * 8, hipMemcpyDeviceToHost));
+    set_default_bounds(sb, c->world, c->rank);
+  }
+  c->nnz = m;
+  if (nnz_out) *nnz_out = m;
+  return 0;
+}
+
+int qmfx_set_factors(qmfx_ctx* c, int side, const double* f) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  if (set_dev(c)) return -2;
+  if (int rc = ensure_side_factors(c, side)) return rc;
+  SideBuf& sb = c->s[side];
+  const size_t n = (size_t)sb.n, kp = c->kp, k = c->k;
+  if (c->prec == 32) {
+    std::vector<float> h(n * kp, 0.f);
+    for (size_t r = 0; r < n; ++r)
+      for (size_t j = 0; j < k; ++j) h[r * kp + j] = (float)f[r * k + j];
+    HIPCHK(scopy(c, sb.F, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  } else {
+    std::vector<double> h(n * kp, 0.0);
+    for (size_t r = 0; r < n; ++r)
+      for (size_t j = 0; j < k; ++j) h[r * kp + j] = f[r * k + j];
+    HIPCHK(scopy(c, sb.F, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int qmfx_get_factors(qmfx_ctx* c, int side, double* f) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  if (set_dev(c)) return -2;
+  if (int rc = ensure_side_factors(c, side)) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  SideBuf& sb = c->s[side];
+  const size_t n = (size_t)sb.n, kp = c->kp, k = c->k;
+  if (c->prec == 32) {
+    std::vector<float> h(n * kp);
+    HIPCHK(scopy(c, h.data(), sb.F, h.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < n; ++r)
+      for (size_t j = 0; j < k; ++j) f[r * k + j] = h[r * kp + j];
+  } else {
+    std::vector<double> h(n * kp);
+    HIPCHK(scopy(c, h.data(), sb.F, h.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < n; ++r)
+      for (size_t j = 0; j < k; ++j) f[r * k + j] = h[r * kp + j];
+  }
+  return 0;
+}
+
+int qmfx_fill_uniform(qmfx_ctx* c, int side, double bound, uint64_t seed) {
+  if (set_dev(c)) return -2;
+  if (int rc = ensure_side_factors(c, side)) return rc;
+  SideBuf& sb = c->s[side];
+  if (c->prec == 32)
+    HIPCHK(launch_fill_uniform_f32((float*)sb.F, sb.n, c->kp, c->k, bound, seed, c->stream));
+  else
+    HIPCHK(launch_fill_uniform_f64((double*)sb.F, sb.n, c->kp, c->k, bound, seed, c->stream));
+  return 0;
+}
+
+int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* loss_sum) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  SideBuf& L = c->s[side];
+  SideBuf& R = c->s[1 - side];
+  if (!L.rowptr) return fail("no interactions uploaded for the solved side");
+  if (set_dev(c)) return -2;
+  if (int rc = ensure_side_factors(c, side)) return rc;
+  if (int rc = ensure_side_factors(c, 1 - side)) return rc;
+  if (int rc = ensure_rowloss(c, L.n)) return rc;
+  const int64_t rb = L.rbeg, re = L.rend, nrows = re - rb;
+  // G = YᵀY of the fixed side (full replica on every rank)
+  if (c->prec == 32)
+    HIPCHK(launch_gram_f32((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart, c->gpart_blocks,
+                           c->stream));
+  else
+    HIPCHK(launch_gram_f64((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
+                           c->gpart_blocks, c->stream));
+  HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (c->prec == 32) {
+    SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
+                       (float*)L.F, c->rowloss, c->status, nullptr, rb, nrows,
+                       (float)alpha, (float)lambda, c->k};
+    HIPCHK(launch_wals_solve_f32(a, c->nt, c->stream));
+  } else {
+    SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
+                        (const double*)c->G, (double*)L.F, c->rowloss, c->status, nullptr, rb,
+                        nrows, alpha, lambda, c->k};
+    HIPCHK(launch_wals_solve_f64(a, c->nt, c->stream));
+  }
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  HIPCHK(launch_sum_f64(c->rowloss + rb, nrows, c->dsum, c->stream));
+  if (c->comm && c->world > 1) {
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < c->world; ++r) {
+      const int64_t b = L.bounds[r], e = L.bounds[r + 1];
+      if (e <= b) continue;
+      char* base = (char*)L.F + (size_t)b * c->kp * c->esz;
+      NCCLCHK(ncclBroadcast(base, base, (size_t)(e - b) * c->kp, nccl_type(c->prec), r, c->comm,
+                            c->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+    NCCLCHK(ncclAllReduce(c->dsum, c->dsum, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->solve_ms += ms;
+  c->solve_launches += 1;
+  {
+    const double k = c->k, s = (double)c->esz;
+    const double nz = (double)(L.h_rowptr[re] - L.h_rowptr[rb]);
+    const double n = (double)nrows;
+    c->solve_flops += nz * k * (k + 1) + nz * 2 * k + n * (k * k * k / 3.0 + 2 * k * k);
+    c->solve_bytes += nz * (4 + s) + nz * k * s + n * k * s + (n + 1) * 8;
+  }
+  c->last_side = side;
+  if (loss_sum) *loss_sum = *c->hsum;
+  return 0;
+}
+
+int qmfx_wals_failed_rows(qmfx_ctx* c, int64_t* rows, int64_t cap, int64_t* count) {
+  SideBuf& L = c->s[c->last_side];
+  if (set_dev(c)) return -2;
+  std::vector<int32_t> st((size_t)std::max<int64_t>(L.n, 1));
+  HIPCHK(scopy(c, st.data(), c->status, st.size() * 4, hipMemcpyDeviceToHost));
+  int64_t cnt = 0;
+  for (int64_t r = 0; r < L.n; ++r)
+    if (st[r]) {
+      if (cnt < cap && rows) rows[cnt] = r;
+      ++cnt;
+    }
+  *count = cnt;
+  return 0;
+}
+
+int qmfx_wals_row_system(qmfx_ctx* c, int side, int64_t row, double alpha, double lambda,
+                         double* A, double* b, double* csum) {
+  SideBuf& L = c->s[side];
+  SideBuf& R = c->s[1 - side];
+  if (row < 0 || row >= L.n) return fail("row out of range");
+  if (set_dev(c)) return -2;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int k = c->k, kp = c->kp;
+  // G of the fixed side as used by the last half: recompute to be safe
+  std::vector<double> G((size_t)kp * kp);
+  if (c->prec == 32) {
+    std::vector<float> g((size_t)kp * kp);
+    HIPCHK(scopy(c, g.data(), c->G, g.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < g.size(); ++i) G[i] = g[i];
+  } else {
+    HIPCHK(scopy(c, G.data(), c->G, G.size() * 8, hipMemcpyDeviceToHost));
+  }
+  const int64_t rb = L.h_rowptr[row], re = L.h_rowptr[row + 1];
+  std::vector<int32_t> cols((size_t)(re - rb));
+  std::vector<double> vals((size_t)(re - rb));
+  if (re > rb) {
+    HIPCHK(scopy(c, cols.data(), L.col + rb, cols.size() * 4, hipMemcpyDeviceToHost));
+    if (c->prec == 32) {
+      std::vector<float> v(vals.size());
+      HIPCHK(scopy(c, v.data(), (float*)L.val + rb, v.size() * 4, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < v.size(); ++i) vals[i] = v[i];
+    } else {
+      HIPCHK(scopy(c, vals.data(), (double*)L.val + rb, vals.size() * 8, hipMemcpyDeviceToHost));
+    }
+  }
+  for (int i = 0; i < k; ++i) {
+    b[i] = 0.0;
+    for (int j = 0; j < k; ++j) A[i * k + j] = G[(size_t)i * kp + j];
+  }
+  double cs = 0.0;
+  std::vector<double> y(k);
+  for (size_t e = 0; e < cols.size(); ++e) {
+    if (c->prec == 32) {
+      std::vector<float> yf(kp);
+      HIPCHK(scopy(c, yf.data(), (float*)R.F + (size_t)cols[e] * kp, kp * 4, hipMemcpyDeviceToHost));
+      for (int i = 0; i < k; ++i) y[i] = yf[i];
+    } else {
+      std::vector<double> yd(kp);
+      HIPCHK(scopy(c, yd.data(), (double*)R.F + (size_t)cols[e] * kp, kp * 8, hipMemcpyDeviceToHost));
+      for (int i = 0; i < k; ++i) y[i] = yd[i];
+    }
+    for (int i = 0; i < k; ++i) {
+      b[i] += y[i] * (1.0 + alpha * vals[e]);
+      for (int j = 0; j < k; ++j) A[i * k + j] += y[i] * alpha * vals[e] * y[j];
+    }
+    cs += 1.0 + alpha * vals[e];
+  }
+  for (int i = 0; i < k; ++i) A[i * k + i] += lambda;
+  if (csum) *csum = cs;
+  return 0;
+}
+
+int qmfx_wals_set_row(qmfx_ctx* c, int side, int64_t row, const double* x) {
+  SideBuf& L = c->s[side];
+  if (row < 0 || row >= L.n) return fail("row out of range");
+  if (set_dev(c)) return -2;
+  const int kp = c->kp, k = c->k;
+  if (c->prec == 32) {
+    std::vector<float> h(kp, 0.f);
+    for (int i = 0; i < k; ++i) h[i] = (float)x[i];
+    HIPCHK(scopy(c, (float*)L.F + (size_t)row * kp, h.data(), kp * 4, hipMemcpyHostToDevice));
+  } else {
+    std::vector<double> h(kp, 0.0);
+    for (int i = 0; i < k; ++i) h[i] = x[i];
+    HIPCHK(scopy(c, (double*)L.F + (size_t)row * kp, h.data(), kp * 8, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+// ---- BPR ------------------------------------------------------------------------------------
+int qmfx_bpr_set_positives(qmfx_ctx* c, const int64_t* users, const int64_t* items, int64_t npos) {
+  const int64_t nu = c->s[0].n, ni = c->s[1].n;
+  if (nu <= 0 || ni <= 0) return fail("shape not set (qmfx_set_shape)");
+  if (set_dev(c)) return -2;
+  std::vector<int32_t> it((size_t)std::max<int64_t>(npos, 1));
+  for (int64_t e = 0; e < npos; ++e) {
+    if (users[e] < 0 || users[e] >= nu || items[e] < 0 || items[e] >= ni)
+      return fail("positive index out of range");
+    it[e] = (int32_t)items[e];
+  }
+  dfree_t(c->pos_user);
+  dfree_t(c->pos_item);
+  dfree_t(c->urowptr);
+  dfree_t(c->uitems);
+  HIPCHK(hipMalloc(&c->pos_user, (size_t)std::max<int64_t>(npos, 1) * 8));
+  HIPCHK(hipMalloc(&c->pos_item, (size_t)std::max<int64_t>(npos, 1) * 4));
+  if (npos > 0) {
+    HIPCHK(scopy(c, c->pos_user, users, (size_t)npos * 8, hipMemcpyHostToDevice));
+    HIPCHK(scopy(c, c->pos_item, it.data(), (size_t)npos * 4, hipMemcpyHostToDevice));
+  }
+  // per-user sorted positive items (the reference's itemMap_, BPREngine.cpp:79-82)
+  std::vector<uint64_t> keys((size_t)npos);
+  for (int64_t e = 0; e < npos; ++e) keys[e] = (uint64_t)users[e] * (uint64_t)ni + (uint64_t)items[e];
+  std::sort(keys.begin(), keys.end());
+  std::vector<int64_t> rp((size_t)nu + 1, 0);
+  std::vector<int32_t> ui((size_t)std::max<int64_t>(npos, 1));
+  for (int64_t e = 0; e < npos; ++e) {
+    rp[keys[e] / ni + 1]++;
+    ui[e] = (int32_t)(keys[e] % ni);
+  }
+  for (int64_t u = 0; u < nu; ++u) rp[u + 1] += rp[u];
+  HIPCHK(hipMalloc(&c->urowptr, (size_t)(nu + 1) * 8));
+  HIPCHK(hipMalloc(&c->uitems, ui.size() * 4));
+  HIPCHK(scopy(c, c->urowptr, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(scopy(c, c->uitems, ui.data(), ui.size() * 4, hipMemcpyHostToDevice));
+  c->npos = npos;
+  if (int rc = ensure_side_factors(c, 0)) return rc;
+  if (int rc = ensure_side_factors(c, 1)) return rc;
+  if (!c->bias) {
+    HIPCHK(hipMalloc(&c->bias, (size_t)ni * c->esz));
+    HIPCHK(hipMemsetAsync(c->bias, 0, (size_t)ni * c->esz, c->stream));
+  }
+  return 0;
+}
+
+int qmfx_bpr_set_biases(qmfx_ctx* c, const double* bias) {
+  const int64_t ni = c->s[1].n;
+  if (ni <= 0) return fail("shape not set");
+  if (set_dev(c)) return -2;
+  if (!c->bias) HIPCHK(hipMalloc(&c->bias, (size_t)ni * c->esz));
+  if (c->prec == 32) {
+    auto v = convert<float>(bias, (size_t)ni);
+    HIPCHK(scopy(c, c->bias, v.data(), (size_t)ni * 4, hipMemcpyHostToDevice));
+  } else {
+    HIPCHK(scopy(c, c->bias, bias, (size_t)ni * 8, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int qmfx_bpr_get_biases(qmfx_ctx* c, double* bias) {
+  const int64_t ni = c->s[1].n;
+  if (!c->bias) return fail("no biases");
+  if (set_dev(c)) return -2;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->prec == 32) {
+    std::vector<float> v((size_t)ni);
+    HIPCHK(scopy(c, v.data(), c->bias, (size_t)ni * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < ni; ++i) bias[i] = v[i];
+  } else {
+    HIPCHK(scopy(c, bias, c->bias, (size_t)ni * 8, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+static uint64_t gcd64(uint64_t a, uint64_t b) {
+  while (b) {
+    uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+template <typename T>
+static BprArgs<T> bpr_args(qmfx_ctx* c, double lr, double bl, double ul, double il, int ub) {
+  BprArgs<T> a{};
+  a.U = (T*)c->s[0].F;
+  a.I = (T*)c->s[1].F;
+  a.bias = (T*)c->bias;
+  a.pos_user = c->pos_user;
+  a.pos_item = c->pos_item;
+  a.npos = c->npos;
+  a.urowptr = c->urowptr;
+  a.uitems = c->uitems;
+  a.nitems = c->s[1].n;
+  a.lr = (T)lr;
+  a.bias_lambda = (T)bl;
+  a.user_lambda = (T)ul;
+  a.item_lambda = (T)il;
+  a.use_biases = ub;
+  a.kp = c->kp;
+  a.bad = c->bad;
+  return a;
+}
+
+extern "C" {
+
+int qmfx_bpr_epoch(qmfx_ctx* c, uint64_t seed, int num_neg, double lr, double bias_lambda,
+                   double user_lambda, double item_lambda, int use_biases, int shuffle) {
+  if (!c->pos_user) return fail("no positives (qmfx_bpr_set_positives)");
+  if (c->npos == 0) return 0;
+  if (set_dev(c)) return -2;
+  uint64_t pa = 1, pb = 0;
+  if (shuffle) {
+    pa = (mix64(seed ^ 0xa5a5a5a5ull) % (uint64_t)c->npos) | 1ull;
+    while (gcd64(pa, (uint64_t)c->npos) != 1) pa += 2;
+    pa %= (uint64_t)c->npos;
+    if (pa == 0) pa = 1;
+    pb = mix64(seed ^ 0x5a5a5a5aull) % (uint64_t)c->npos;
+  }
+  HIPCHK(hipMemsetAsync(c->bad, 0, 4, c->stream));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (c->prec == 32) {
+    auto a = bpr_args<float>(c, lr, bias_lambda, user_lambda, item_lambda, use_biases);
+    a.num_neg = num_neg;
+    a.seed = seed;
+    a.perm_a = pa;
+    a.perm_b = pb;
+    HIPCHK(launch_bpr_epoch_f32(a, c->kp, c->stream));
+  } else {
+    auto a = bpr_args<double>(c, lr, bias_lambda, user_lambda, item_lambda, use_biases);
+    a.num_neg = num_neg;
+    a.seed = seed;
+    a.perm_a = pa;
+    a.perm_b = pb;
+    HIPCHK(launch_bpr_epoch_f64(a, c->kp, c->stream));
+  }
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  int32_t bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, c->bad, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->solve_ms += ms;
+  c->solve_launches += 1;
+  const double upd = (double)c->npos * num_neg;
+  c->solve_flops += upd * 10.0 * c->k;
+  c->solve_bytes += upd * (6.0 * c->k * c->esz + 16 + 40);
+  if (bad) return fail("gradients too big, try decreasing the learning rate (--init_learning_rate)", -4);
+  return 0;
+}
+
+int qmfx_bpr_apply(qmfx_ctx* c, const int64_t* trip, int64_t n, double lr, double bias_lambda,
+                   double user_lambda, double item_lambda, int use_biases) {
+  if (set_dev(c)) return -2;
+  if (int rc = ensure_side_factors(c, 0)) return rc;
+  if (int rc = ensure_side_factors(c, 1)) return rc;
+  if (!c->bias) {
+    HIPCHK(hipMalloc(&c->bias, (size_t)c->s[1].n * c->esz));
+    HIPCHK(hipMemsetAsync(c->bias, 0, (size_t)c->s[1].n * c->esz, c->stream));
+  }
+  for (int64_t t = 0; t < n; ++t)
+    if (trip[3 * t] < 0 || trip[3 * t] >= c->s[0].n || trip[3 * t + 1] < 0 ||
+        trip[3 * t + 1] >= c->s[1].n || trip[3 * t + 2] < 0 || trip[3 * t + 2] >= c->s[1].n)
+      return fail("triplet index out of range");
+  int64_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, (size_t)std::max<int64_t>(n, 1) * 24));
+  HIPCHK(scopy(c, d, trip, (size_t)n * 24, hipMemcpyHostToDevice));
+  HIPCHK(hipMemsetAsync(c->bad, 0, 4, c->stream));
+  if (c->prec == 32) {
+    auto a = bpr_args<float>(c, lr, bias_lambda, user_lambda, item_lambda, use_biases);
+    HIPCHK(launch_bpr_apply_f32(a, d, n, c->kp, c->stream));
+  } else {
+    auto a = bpr_args<double>(c, lr, bias_lambda, user_lambda, item_lambda, use_biases);
+    HIPCHK(launch_bpr_apply_f64(a, d, n, c->kp, c->stream));
+  }
+  int32_t bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, c->bad, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  hipFree(d);
+  if (bad) return fail("gradients too big, try decreasing the learning rate (--init_learning_rate)", -4);
+  return 0;
+}
+
+int qmfx_bpr_eval(qmfx_ctx* c, int slot, const int64_t* trip, int64_t n, int use_biases,
+                  double* loss_sum) {
+  if (slot != 0 && slot != 1) return fail("slot must be 0 or 1");
+  if (set_dev(c)) return -2;
+  if (c->trip_src[slot] != (const void*)trip || c->trip_n[slot] != n) {
+    for (int64_t t = 0; t < n; ++t)
+      if (trip[3 * t] < 0 || trip[3 * t] >= c->s[0].n || trip[3 * t + 1] < 0 ||
+          trip[3 * t + 1] >= c->s[1].n || trip[3 * t + 2] < 0 || trip[3 * t + 2] >= c->s[1].n)
+        return fail("triplet index out of range");
+    dfree_t(c->trip[slot]);
+    HIPCHK(hipMalloc(&c->trip[slot], (size_t)std::max<int64_t>(n, 1) * 24));
+    HIPCHK(scopy(c, c->trip[slot], trip, (size_t)n * 24, hipMemcpyHostToDevice));
+    c->trip_src[slot] = trip;
+    c->trip_n[slot] = n;
+  }
+  if (c->prec == 32)
+    HIPCHK(launch_bpr_eval_f32((const float*)c->s[0].F, (const float*)c->s[1].F,
+                               (const float*)c->bias, c->trip[slot], n, c->kp, use_biases,
+                               c->eval_partial, c->dsum, c->stream));
+  else
+    HIPCHK(launch_bpr_eval_f64((const double*)c->s[0].F, (const double*)c->s[1].F,
+                               (const double*)c->bias, c->trip[slot], n, c->kp, use_biases,
+                               c->eval_partial, c->dsum, c->stream));
+  HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *loss_sum = *c->hsum;
+  return 0;
+}
+
+// ---- multi-GPU -----------------------------------------------------------------------------
+int qmfx_rccl_unique_id(uint8_t* id128) {
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  std::memcpy(id128, &id, 128);
+  return 0;
+}
+
+int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
+  if (world < 1 || rank < 0 || rank >= world) return fail("bad rank/world");
+  if (set_dev(c)) return -2;
+  c->rank = rank;
+  c->world = world;
+  if (world > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, id128, 128);
+    NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
+  }
+  for (auto& sb : c->s)
+    if (!sb.h_rowptr.empty()) set_default_bounds(sb, world, rank);
+  return 0;
+}
+
+int qmfx_partition_rows(const int64_t* rowptr, int64_t nrows, int world, int rank,
+                        int64_t* begin, int64_t* end) {
+  if (world < 1 || rank < 0 || rank >= world) return fail("bad rank/world");
+  SideBuf sb;
+  sb.n = nrows;
+  sb.h_rowptr.assign(rowptr, rowptr + nrows + 1);
+  set_default_bounds(sb, world, rank);
+  *begin = sb.rbeg;
+  *end = sb.rend;
+  return 0;
+}
+
+// ---- measurement ---------------------------------------------------------------------------
+int qmfx_solve_kernel_stats(qmfx_ctx* c, double* total_ms, int64_t* launches, double* flops,
+                            double* bytes) {
+  if (total_ms) *total_ms = c->solve_ms;
+  if (launches) *launches = c->solve_launches;
+  if (flops) *flops = c->solve_flops;
+  if (bytes) *bytes = c->solve_bytes;
+  return 0;
+}
+
+int qmfx_reset_stats(qmfx_ctx* c) {
+  c->solve_ms = c->solve_flops = c->solve_bytes = 0;
+  c->solve_launches = 0;
+  return 0;
+}
+
+int qmfx_selftest_mfma(int device, int precision, const double* A, const double* B, double* C) {
+  HIPCHK(hipSetDevice(device));
+  const size_t es = precision == 32 ? 4 : 8;
+  void *dA, *dB, *dC;
+  HIPCHK(hipMalloc(&dA, 64 * es));
+  HIPCHK(hipMalloc(&dB, 64 * es));
+  HIPCHK(hipMalloc(&dC, 256 * es));
+  if (precision == 32) {
+    auto a = convert<float>(A, 64), b = convert<float>(B, 64);
+    HIPCHK(hipMemcpy(dA, a.data(), 256, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dB, b.data(), 256, hipMemcpyHostToDevice));
+    HIPCHK(launch_mfma_selftest_f32((float*)dA, (float*)dB, (float*)dC, nullptr));
+    std::vector<float> cc(256);
+    HIPCHK(hipMemcpy(cc.data(), dC, 1024, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 256; ++i) C[i] = cc[i];
+  } else {
+    HIPCHK(hipMemcpy(dA, A, 512, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dB, B, 512, hipMemcpyHostToDevice));
+    HIPCHK(launch_mfma_selftest_f64((double*)dA, (double*)dB, (double*)dC, nullptr));
+    HIPCHK(hipMemcpy(C, dC, 2048, hipMemcpyDeviceToHost));
+  }
+  hipFree(dA);
+  hipFree(dB);
+  hipFree(dC);
+  return 0;
+}
+
+}  // extern "C"

@@ -45,3 +45,22 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def csr_from_triples(users, items, values):
+    """Independent numpy restatement of groupSignals (WALSEngine.cpp:130-163): ids sorted
+    ascending as signed int64 give idx 0..n-1; each row's signals sorted by the other id;
+    duplicates kept.  Returns (uids, iids, (urp, ucol, uval), (irp, icol, ival))."""
+    users = np.asarray(users, np.int64)
+    items = np.asarray(items, np.int64)
+    values = np.asarray(values, np.float64)
+    uids, uidx = np.unique(users, return_inverse=True)
+    iids, iidx = np.unique(items, return_inverse=True)
+
+    def side(rows, cols, nrows):
+        order = np.lexsort((cols, rows))  # stable: by row, then col
+        rp = np.zeros(nrows + 1, np.int64)
+        np.add.at(rp, rows + 1, 1)
+        return np.cumsum(rp), cols[order].astype(np.int32), values[order]
+
+    return uids, iids, side(uidx, iidx, len(uids)), side(iidx, uidx, len(iids))

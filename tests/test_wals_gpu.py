@@ -1,0 +1,147 @@
+"""WALS parity on the MI355X: the HIP path (through the C ABI) against the CPU oracle on
+identical inputs and initial factors.
+
+Tolerances (BASELINE.json north_star: factors within 1e-4 relative; index/ID bookkeeping
+bit-exact): fp64 path 1e-9 normwise-relative per half step (only rounding differs: MFMA
+accumulation order and Cholesky vs Bunch-Kaufman), fp32 path 1e-4.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as po
+import qmf_amd
+from helpers import csr_from_triples, load_ml100k, load_tiny, rel_err, synth
+
+pytestmark = pytest.mark.gpu
+
+LAM, ALPHA = 0.05, 40.0
+
+
+def make_pair(users, items, values, k, precision, init=None, seed=0, lam=LAM, alpha=ALPHA):
+    """(oracle, device context) on the same dataset with identical item-factor init."""
+    o = po.OracleWALS(users, items, values, k, lam, alpha)
+    uids, iids, (urp, ucol, uval), (irp, icol, ival) = csr_from_triples(users, items, values)
+    # bookkeeping: the independent numpy CSR must equal the oracle's (bit-exact)
+    assert np.array_equal(uids, o.ids(0)) and np.array_equal(iids, o.ids(1))
+    for side, (rp, col, val) in ((0, (urp, ucol, uval)), (1, (irp, icol, ival))):
+        orp, ocol, oval = o.csr(side)
+        assert np.array_equal(orp, rp) and np.array_equal(ocol, col)
+        # std::sort leaves the order of duplicate (u, i) pairs unspecified: compare the
+        # values of duplicates as multisets
+        row = np.repeat(np.arange(len(rp) - 1), np.diff(rp))
+        a = np.lexsort((oval, ocol, row))
+        b = np.lexsort((val, col, row))
+        assert np.array_equal(oval[a], val[b])
+    c = qmf_amd.Context(k, precision)
+    c.set_shape(len(uids), len(iids))
+    c.upload_csr(0, urp, ucol, uval)
+    c.upload_csr(1, irp, icol, ival)
+    if init is None:
+        init = np.random.default_rng(seed).uniform(-0.01, 0.01, (len(iids), k))
+    o.set_factors(1, init)
+    c.set_factors(1, init)
+    return o, c
+
+
+def test_mfma_layout_f32_f64():
+    rng = np.random.default_rng(0)
+    A = rng.integers(-8, 8, (16, 4)).astype(np.float64)
+    B = rng.integers(-8, 8, (4, 16)).astype(np.float64)
+    for prec in (32, 64):
+        np.testing.assert_array_equal(qmf_amd.selftest_mfma(prec, A, B), A @ B)
+
+
+@pytest.mark.parametrize("precision,tol,lam", [(64, 1e-9, LAM), (32, 1e-4, 5.0)])
+@pytest.mark.parametrize("k", [8, 16, 30])
+def test_tiny_half_steps(precision, tol, lam, k):
+    # The tiny fixture has 9 users: with λ = 0.05 its item systems have cond ≈ 1e4–1e5,
+    # beyond what fp32 factors can resolve to 1e-4 (fp32 error ≈ cond·6e-8).  fp64 is
+    # checked at the reference λ; fp32 at a well-conditioned λ.
+    u, i, v = load_tiny()
+    o, c = make_pair(u, i, v, k, precision, seed=k, lam=lam)
+    for epoch in range(2):
+        for side in (0, 1):
+            lo = o.iterate(side)
+            ld = c.wals_half(side, ALPHA, lam) / (o.nusers * o.nitems)
+            assert rel_err(c.factors(side), o.factors(side)) < tol
+            assert abs(ld - lo) <= tol * max(1.0, abs(lo)) * 10
+            # keep the two in lock-step for the next half
+            c.set_factors(side, o.factors(side))
+
+
+@pytest.mark.parametrize("precision,tol", [(64, 1e-9), (32, 1e-4)])
+def test_ml100k_shape_ten_epochs(precision, tol):
+    """The survey's reference-pinned dataset: 10 epochs run
+    independently on both sides; factors and the per-epoch loss must track the oracle."""
+    d = load_ml100k()
+    k = 30
+    init = d["init"][: 1682 * k].reshape(1682, k)
+    o, c = make_pair(d["users"], d["items"], d["values"], k, precision, init=init)
+    ol = o.optimize(10, 4)
+    dl = []
+    for _ in range(10):
+        c.wals_half(0, ALPHA, LAM)
+        dl.append(c.wals_half(1, ALPHA, LAM) / (o.nusers * o.nitems))
+    assert abs(dl[0] - float(d["ref_loss_epoch1"])) < 5e-6 * (1 if precision == 64 else 10)
+    assert abs(dl[9] - float(d["ref_loss_epoch10"])) < 5e-7 * (1 if precision == 64 else 100)
+    np.testing.assert_allclose(dl, ol, rtol=tol * 10)
+    assert rel_err(c.factors(0), o.factors(0)) < tol * 10
+    assert rel_err(c.factors(1), o.factors(1)) < tol * 10
+
+
+@pytest.mark.parametrize("k", [32, 64, 96, 128])
+def test_synthetic_fp32_one_epoch(k):
+    u, i, v = synth(3000, 700, 40000, seed=k)
+    o, c = make_pair(u, i, v, k, 32, seed=1)
+    for side in (0, 1):
+        lo = o.iterate(side)
+        ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+        assert rel_err(c.factors(side), o.factors(side)) < 1e-4
+        assert abs(ld - lo) < 1e-4 * abs(lo)
+
+
+def test_single_signal_rows_and_tails():
+    # rows with 1..9 signals exercise every k-step tail of the 4-wide MFMA loop
+    users, items = [], []
+    for r in range(1, 10):
+        for j in range(r):
+            users.append(r)
+            items.append((r * 7 + j * 3) % 23)
+    v = np.arange(len(users)) % 5 + 1.0
+    o, c = make_pair(users, items, v, 8, 64, seed=3)
+    o.iterate(0)
+    c.wals_half(0, ALPHA, LAM)
+    assert rel_err(c.factors(0), o.factors(0)) < 1e-10
+
+
+def test_update_factors_for_one_known_answer():
+    # WALSEngineTest.cpp:145-205 through the device path: Y ≡ 0.1, α = λ = 1 → x = 0.4/1.12
+    c = qmf_amd.Context(3, 64)
+    c.set_shape(1, 2)
+    c.upload_csr(0, [0, 2], [0, 1], [1.0, 1.0])
+    c.upload_csr(1, [0, 1, 2], [0, 0], [1.0, 1.0])
+    c.set_factors(1, np.full((2, 3), 0.1))
+    c.wals_half(0, 1.0, 1.0)
+    np.testing.assert_allclose(c.factors(0), np.full((1, 3), 0.4 / 1.12), rtol=1e-12)
+
+
+def test_zero_and_negative_values_spd_path():
+    # value 0 contributes only to b (c = 1), never to A; still SPD
+    u, i, v = load_tiny()
+    assert (v == 0).any()
+    o, c = make_pair(u, i, v, 8, 64, seed=5)
+    o.iterate(0)
+    c.wals_half(0, ALPHA, LAM)
+    assert len(c.failed_rows()) == 0
+    assert rel_err(c.factors(0), o.factors(0)) < 1e-9
+
+
+def test_indefinite_rows_are_flagged():
+    # 1 + α·v < 0 makes some systems indefinite: the device must flag them, not return
+    # garbage silently (the C++ engine then re-solves them with Bunch-Kaufman on the host).
+    u = np.array([0, 0, 0, 1, 1, 2])
+    i = np.array([0, 1, 2, 0, 2, 1])
+    v = np.array([-5.0, -5.0, -5.0, 1.0, 2.0, 1.0])
+    o, c = make_pair(u, i, v, 8, 64, init=np.full((3, 8), 0.3), lam=0.01, alpha=40.0)
+    c.wals_half(0, 40.0, 0.01)
+    assert 0 in set(c.failed_rows().tolist())
