@@ -146,13 +146,31 @@ def main():
     ms_epoch = el / args.steps * 1e3
     solves = (nu + ni) * args.steps
     value = solves / el
-    # roofline of the dominant kernel (fused row solve): compute-bound at k=128
-    launch_s = st["ms"] / 1e3 / max(st["launches"], 1)
-    fl_launch = st["flops"] / max(st["launches"], 1)
-    by_launch = st["bytes"] / max(st["launches"], 1)
-    peak = PEAK_F32_TFLOPS if args.precision == 32 else PEAK_F64_TFLOPS
-    achieved_tf = fl_launch / launch_s / 1e12
-    hbm_gbs = by_launch / launch_s / 1e9
+    peak_tf = PEAK_F32_TFLOPS if args.precision == 32 else PEAK_F64_TFLOPS
+    ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
+    classes = {}
+    for cls, name in ((0, "wals_direct_kernel"), (1, "wals_whitened (row solve + unwhiten)")):
+        ks = ctx.kernel_stats(cls)
+        if ks["launches"] == 0 or ks["ms"] <= 0:
+            continue
+        sec = ks["ms"] / 1e3 / ks["launches"]
+        fl = ks["flops"] / ks["launches"]
+        by = ks["bytes"] / ks["launches"]
+        classes[name] = dict(launch_ms=round(sec * 1e3, 3), tflops=round(fl / sec / 1e12, 3),
+                             gbs=round(by / sec / 1e9, 1), flops_per_launch=fl,
+                             bytes_per_launch=by, total_ms=round(ks["ms"], 3))
+    dom = max(classes, key=lambda n: classes[n]["total_ms"])
+    d = classes[dom]
+    if d["flops_per_launch"] / d["bytes_per_launch"] >= ridge:
+        roof = {"kernel": dom, "bound": "mfma", "achieved": d["tflops"], "peak": peak_tf,
+                "unit": "TFLOP/s", "frac": round(d["tflops"] / peak_tf, 4)}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": d["gbs"], "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(d["gbs"] / PEAK_HBM_GBS, 4)}
+    roof.update({"traffic": None, "launch_ms": d["launch_ms"], "classes": classes})
+    half = ctx.kernel_stats(2)
+    epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
+    hbm_frac_epoch = epoch_bytes / (ms_epoch / 1e3) / (PEAK_HBM_GBS * 1e9)
     if rank != 0:
         return
     out = {
@@ -172,12 +190,8 @@ def main():
                    % (args.config, nu, ni, nnz, k, LAM, ALPHA),
                    "nusers": nu, "nitems": ni, "nnz": nnz, "nfactors": k,
                    "parallelism": "rows%d" % world},
-        "roofline": {"kernel": "wals_solve_kernel", "bound": "mfma", "achieved": round(achieved_tf, 3),
-                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved_tf / peak, 4),
-                     "traffic": None, "launch_ms": round(launch_s * 1e3, 3),
-                     "hbm_achieved_GBs": round(hbm_gbs, 1),
-                     "hbm_frac": round(hbm_gbs / PEAK_HBM_GBS, 4),
-                     "alg_flops_per_launch": fl_launch, "alg_bytes_per_launch": by_launch},
+        "roofline": roof,
+        "hbm_roofline_frac_epoch": round(hbm_frac_epoch, 4),
         "loss": loss / nu / ni,
     }
     if not args.no_cpu_baseline and world == 1:

@@ -113,6 +113,11 @@ int qmfx_partition_rows(const int64_t* rowptr, int64_t nrows, int world, int ran
 /* HIP-event time of the row-solve kernel launches (on the context stream) since reset. */
 int qmfx_solve_kernel_stats(qmfx_ctx* ctx, double* total_ms, int64_t* launches,
                             double* flops, double* bytes);
+/* Per kernel class since reset: 0 = direct row kernel, 1 = whitened row kernels (row solve
+ * + unwhitening GEMM), 2 = whole half-epoch (all kernels, collectives included).  flops /
+ * bytes are the algorithmic work of that class (SURVEY.md §8(d) accounting). */
+int qmfx_kernel_stats(qmfx_ctx* ctx, int cls, double* total_ms, int64_t* launches,
+                      double* flops, double* bytes);
 int qmfx_reset_stats(qmfx_ctx* ctx);
 
 /* ---- self tests ------------------------------------------------------------------------------ */

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libqmfx.so")
+LIB_PATH = os.environ.get("QMFX_LIB") or os.path.join(_HERE, "_build", "libqmfx.so")
 
 c_i64 = ctypes.c_int64
 c_u64 = ctypes.c_uint64
@@ -52,6 +52,7 @@ SIGNATURES = {
     "qmfx_dist_init": [vp, c_int, c_int, P_u8],
     "qmfx_partition_rows": [P_i64, c_i64, c_int, c_int, P_i64, P_i64],
     "qmfx_solve_kernel_stats": [vp, P_f64, P_i64, P_f64, P_f64],
+    "qmfx_kernel_stats": [vp, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_reset_stats": [vp],
     "qmfx_selftest_mfma": [c_int, c_int, P_f64, P_f64, P_f64],
 }
@@ -258,6 +259,12 @@ class Context:
         ms, n, fl, by = c_dbl(), c_i64(), c_dbl(), c_dbl()
         _check(lib().qmfx_solve_kernel_stats(self.h, ctypes.byref(ms), ctypes.byref(n),
                                              ctypes.byref(fl), ctypes.byref(by)))
+        return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
+
+    def kernel_stats(self, cls):
+        ms, n, fl, by = c_dbl(), c_i64(), c_dbl(), c_dbl()
+        _check(lib().qmfx_kernel_stats(self.h, cls, ctypes.byref(ms), ctypes.byref(n),
+                                       ctypes.byref(fl), ctypes.byref(by)))
         return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
 
     def reset_stats(self):

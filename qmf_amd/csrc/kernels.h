@@ -21,14 +21,28 @@ struct SolveArgs {
   T alpha;
   T lambda;
   int k;                  // real number of factors (≤ KP)
+  int ablate;             // timing experiments only: bit0 skip Gram loop, bit1 skip panel
+                          // factorization, bit2 skip trailing MFMA update, bit3 skip backward
 };
 
-hipError_t launch_wals_solve_f32(const SolveArgs<float>& a, int nt, hipStream_t s);
-hipError_t launch_wals_solve_f64(const SolveArgs<double>& a, int nt, hipStream_t s);
-hipError_t launch_gram_f32(const float* Y, int64_t n, int nt, float* G, double* partial,
-                           int max_blocks, hipStream_t s);
-hipError_t launch_gram_f64(const double* Y, int64_t n, int nt, double* G, double* partial,
-                           int max_blocks, hipStream_t s);
+hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s);
+hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s);
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
+hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,
+                         int nt, const float* Linv, double* rowloss, double lambda,
+                         bool unwhiten, hipStream_t s);
+hipError_t launch_whiten(const double* in, double* out, const int64_t* order, int64_t nrows,
+                         int nt, const double* Linv, double* rowloss, double lambda,
+                         bool unwhiten, hipStream_t s);
+hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
+                           int32_t* status, hipStream_t s);
+hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
+                           int32_t* status, hipStream_t s);
+hipError_t launch_gram(const float* Y, int64_t n, int nt, float* G, double* partial,
+                       int max_blocks, hipStream_t s);
+hipError_t launch_gram(const double* Y, int64_t n, int nt, double* G, double* partial,
+                       int max_blocks, hipStream_t s);
 hipError_t launch_sum_f64(const double* x, int64_t n, double* out, hipStream_t s);
 hipError_t launch_mfma_selftest_f32(const float* A, const float* B, float* C, hipStream_t s);
 hipError_t launch_mfma_selftest_f64(const double* A, const double* B, double* C,

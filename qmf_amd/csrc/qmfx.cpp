@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -49,6 +50,14 @@ struct SideBuf {
   std::vector<int64_t> h_rowptr;
   int64_t rbeg = 0, rend = 0;           // rows solved by this rank
   std::vector<int64_t> bounds;          // per-rank row boundaries (world+1)
+  // Row buckets of this rank (device list `order`): [whitened n≤16 | ≤32 | ≤48 | ≤64 |
+  // direct rows, heaviest first].  wb[i]..wb[i+1] = whitened bucket NTN = i+1; wb[4]..n_ord
+  // = direct.  nnz per bucket class for the roofline accounting.
+  int64_t* d_order = nullptr;
+  int64_t wb[5] = {0, 0, 0, 0, 0};
+  int64_t n_ord = 0;
+  double nnz_w = 0, nnz_d = 0;
+  bool buckets_valid = false;
 };
 
 }  // namespace
@@ -89,6 +98,17 @@ struct qmfx_ctx {
   const void* trip_src[2] = {nullptr, nullptr};
   double* eval_partial = nullptr;
   uint64_t bpr_epochs = 0;
+  int ablate = 0;  // QMFX_ABLATE (timing experiments only)
+  bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
+  // whitened path buffers
+  void* Z = nullptr;  // whitened fixed side [max(nu, ni)][kp]
+  int64_t z_cap = 0;
+  void* Linv = nullptr;  // kp × kp
+  int32_t* chol_status = nullptr;
+  // per-class timing: 0 direct kernel, 1 whitened kernels (row solve + unwhiten), 2 whole half
+  hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};
+  double cls_ms[3] = {0, 0, 0}, cls_flops[3] = {0, 0, 0}, cls_bytes[3] = {0, 0, 0};
+  int64_t cls_launches[3] = {0, 0, 0};
 };
 
 namespace {
@@ -165,6 +185,58 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
   return hipStreamSynchronize(c->stream);
 }
 
+// Largest whitened-row bucket (NTN) usable for this factor tiling: n padded to 16 must be
+// at most 64 and at most KP/2 (beyond that the k×k solve is the cheaper one).
+int max_whitened_ntn(const qmfx_ctx* c) {
+  if (!c->whitened_enabled) return 0;
+  int m = c->nt / 2;
+  if (m > 4) m = 4;
+  if (c->prec == 64 && m > 2) m = 2;
+  return m;
+}
+
+// Splits this rank's rows of `side` into whitened buckets (by padded signal count) and the
+// direct bucket (heaviest rows first, for load balance), and uploads the order list.
+int build_buckets(qmfx_ctx* c, int side) {
+  SideBuf& sb = c->s[side];
+  sb.buckets_valid = false;
+  if (sb.h_rowptr.empty()) return 0;
+  const int mx = max_whitened_ntn(c);
+  std::vector<int64_t> wlist[4];
+  std::vector<std::pair<int64_t, int64_t>> direct;
+  double nnz_w = 0, nnz_d = 0;
+  for (int64_t r = sb.rbeg; r < sb.rend; ++r) {
+    const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
+    const int64_t ntn = (std::max<int64_t>(n, 1) + 15) / 16;
+    if (ntn <= mx) {
+      wlist[ntn - 1].push_back(r);
+      nnz_w += (double)n;
+    } else {
+      direct.emplace_back(n, r);
+      nnz_d += (double)n;
+    }
+  }
+  std::stable_sort(direct.begin(), direct.end(),
+                   [](const auto& x, const auto& y) { return x.first > y.first; });
+  std::vector<int64_t> order;
+  order.reserve(sb.rend - sb.rbeg);
+  for (int i = 0; i < 4; ++i) {
+    sb.wb[i] = (int64_t)order.size();
+    order.insert(order.end(), wlist[i].begin(), wlist[i].end());
+  }
+  sb.wb[4] = (int64_t)order.size();
+  for (const auto& d : direct) order.push_back(d.second);
+  sb.n_ord = (int64_t)order.size();
+  sb.nnz_w = nnz_w;
+  sb.nnz_d = nnz_d;
+  if (sb.d_order) (void)hipFree(sb.d_order);
+  sb.d_order = nullptr;
+  HIPCHK(hipMalloc(&sb.d_order, (size_t)std::max<int64_t>(sb.n_ord, 1) * 8));
+  HIPCHK(scopy(c, sb.d_order, order.data(), (size_t)sb.n_ord * 8, hipMemcpyHostToDevice));
+  sb.buckets_valid = true;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -191,6 +263,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->nt = nt;
   c->kp = 16 * nt;
   c->esz = precision == 32 ? 4 : 8;
+  if (const char* ab = std::getenv("QMFX_ABLATE")) c->ablate = std::atoi(ab);
+  if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->G, (size_t)c->kp * c->kp * c->esz);
@@ -202,6 +276,9 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipMalloc(&c->eval_partial, 1024 * sizeof(double));
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->evh[i]);
+  if (e == hipSuccess) e = hipMalloc(&c->Linv, (size_t)c->kp * c->kp * c->esz);
+  if (e == hipSuccess) e = hipMalloc(&c->chol_status, sizeof(int32_t));
   if (e != hipSuccess) {
     g_err = std::string("qmfx_create: ") + hipGetErrorString(e);
     delete c;
@@ -221,6 +298,7 @@ int qmfx_destroy(qmfx_ctx* c) {
     dfree_t(sb.col);
     dfree(sb.val);
     dfree(sb.F);
+    dfree_t(sb.d_order);
   }
   dfree(c->G);
   dfree_t(c->gpart);
@@ -239,6 +317,11 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree_t(c->trip[1]);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  for (auto& ev : c->evh)
+    if (ev) hipEventDestroy(ev);
+  dfree(c->Z);
+  dfree(c->Linv);
+  dfree_t(c->chol_status);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -307,6 +390,7 @@ int qmfx_upload_csr(qmfx_ctx* c, int side, const int64_t* rowptr, const int32_t*
   c->nnz = nnz;
   sb.h_rowptr.assign(rowptr, rowptr + sb.n + 1);
   set_default_bounds(sb, c->world, c->rank);
+  if (int rc = build_buckets(c, side)) return rc;
   return 0;
 }
 
@@ -372,6 +456,7 @@ int qmfx_gen_synthetic(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz,
     sb.h_rowptr.resize(sb.n + 1);
     HIPCHK(scopy(c, sb.h_rowptr.data(), sb.rowptr, (size_t)(sb.n + 1) * 8, hipMemcpyDeviceToHost));
     set_default_bounds(sb, c->world, c->rank);
+    if (int rc = build_buckets(c, side)) return rc;
   }
   c->nnz = m;
   if (nnz_out) *nnz_out = m;
@@ -435,32 +520,85 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   SideBuf& L = c->s[side];
   SideBuf& R = c->s[1 - side];
   if (!L.rowptr) return fail("no interactions uploaded for the solved side");
+  if (!L.buckets_valid) return fail("row buckets not built");
   if (set_dev(c)) return -2;
   if (int rc = ensure_side_factors(c, side)) return rc;
   if (int rc = ensure_side_factors(c, 1 - side)) return rc;
   if (int rc = ensure_rowloss(c, L.n)) return rc;
   const int64_t rb = L.rbeg, re = L.rend, nrows = re - rb;
+  const int64_t nW = L.wb[4];                   // whitened rows (buckets 0..3)
+  const bool use_w = nW > 0 && lambda > 0.0;    // M = YᵀY + λI is SPD only for λ > 0
+  const int64_t d_begin = use_w ? L.wb[4] : 0;  // direct rows in the order list
+  const bool fp32 = c->prec == 32;
+  HIPCHK(hipEventRecord(c->evh[0], c->stream));
   // G = YᵀY of the fixed side (full replica on every rank)
-  if (c->prec == 32)
-    HIPCHK(launch_gram_f32((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart, c->gpart_blocks,
-                           c->stream));
+  if (fp32)
+    HIPCHK(launch_gram((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart, c->gpart_blocks,
+                       c->stream));
   else
-    HIPCHK(launch_gram_f64((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
-                           c->gpart_blocks, c->stream));
+    HIPCHK(launch_gram((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart, c->gpart_blocks,
+                       c->stream));
+  if (use_w) {
+    if (c->z_cap < R.n) {
+      dfree(c->Z);
+      const int64_t cap = std::max(c->s[0].n, c->s[1].n);
+      HIPCHK(hipMalloc(&c->Z, (size_t)cap * c->kp * c->esz));
+      c->z_cap = cap;
+    }
+    HIPCHK(hipMemsetAsync(c->chol_status, 0, 4, c->stream));
+    if (fp32) {
+      HIPCHK(launch_chol_inv((const float*)c->G, c->nt, c->k, lambda, (float*)c->Linv,
+                             c->chol_status, c->stream));
+      HIPCHK(launch_whiten((const float*)R.F, (float*)c->Z, nullptr, R.n, c->nt,
+                           (const float*)c->Linv, nullptr, 0.0, false, c->stream));
+    } else {
+      HIPCHK(launch_chol_inv((const double*)c->G, c->nt, c->k, lambda, (double*)c->Linv,
+                             c->chol_status, c->stream));
+      HIPCHK(launch_whiten((const double*)R.F, (double*)c->Z, nullptr, R.n, c->nt,
+                           (const double*)c->Linv, nullptr, 0.0, false, c->stream));
+    }
+  }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
+  // direct rows (heaviest first)
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  if (c->prec == 32) {
+  const int64_t nD = L.n_ord - d_begin;
+  if (fp32) {
     SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
-                       (float*)L.F, c->rowloss, c->status, nullptr, rb, nrows,
-                       (float)alpha, (float)lambda, c->k};
-    HIPCHK(launch_wals_solve_f32(a, c->nt, c->stream));
+                       (float*)L.F, c->rowloss, c->status, L.d_order, d_begin, nD,
+                       (float)alpha, (float)lambda, c->k, c->ablate};
+    HIPCHK(launch_wals_direct(a, c->nt, c->stream));
   } else {
     SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
-                        (const double*)c->G, (double*)L.F, c->rowloss, c->status, nullptr, rb,
-                        nrows, alpha, lambda, c->k};
-    HIPCHK(launch_wals_solve_f64(a, c->nt, c->stream));
+                        (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
+                        d_begin, nD, alpha, lambda, c->k, c->ablate};
+    HIPCHK(launch_wals_direct(a, c->nt, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
+  // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
+  if (use_w) {
+    for (int b = 0; b < 4; ++b) {
+      const int64_t cnt = L.wb[b + 1] - L.wb[b];
+      if (cnt <= 0) continue;
+      if (fp32) {
+        SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
+                           (float*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
+                           (float)alpha, (float)lambda, c->k, c->ablate};
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+      } else {
+        SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z, nullptr,
+                            (double*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
+                            alpha, lambda, c->k, c->ablate};
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+      }
+    }
+    if (fp32)
+      HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order, nW, c->nt,
+                           (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
+    else
+      HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order, nW, c->nt,
+                           (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
+  }
+  HIPCHK(hipEventRecord(c->evh[1], c->stream));
   HIPCHK(launch_sum_f64(c->rowloss + rb, nrows, c->dsum, c->stream));
   if (c->comm && c->world > 1) {
     NCCLCHK(ncclGroupStart());
@@ -474,19 +612,52 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     NCCLCHK(ncclGroupEnd());
     NCCLCHK(ncclAllReduce(c->dsum, c->dsum, 1, ncclFloat64, ncclSum, c->comm, c->stream));
   }
+  HIPCHK(hipEventRecord(c->evh[2], c->stream));
   HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-  c->solve_ms += ms;
-  c->solve_launches += 1;
-  {
-    const double k = c->k, s = (double)c->esz;
-    const double nz = (double)(L.h_rowptr[re] - L.h_rowptr[rb]);
-    const double n = (double)nrows;
-    c->solve_flops += nz * k * (k + 1) + nz * 2 * k + n * (k * k * k / 3.0 + 2 * k * k);
-    c->solve_bytes += nz * (4 + s) + nz * k * s + n * k * s + (n + 1) * 8;
+  int32_t chol_bad = 0;
+  if (use_w) HIPCHK(hipMemcpy(&chol_bad, c->chol_status, 4, hipMemcpyDeviceToHost));
+  if (chol_bad) return fail("YᵀY + λI is not positive definite", -5);
+  // timing and algorithmic work per kernel class (SURVEY.md §8(d) accounting)
+  float ms_d = 0.f, ms_w = 0.f, ms_h = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms_d, c->ev0, c->ev1));
+  HIPCHK(hipEventElapsedTime(&ms_w, c->ev1, c->evh[1]));
+  HIPCHK(hipEventElapsedTime(&ms_h, c->evh[0], c->evh[2]));
+  const double k = c->k, s = (double)c->esz;
+  const double nzd = use_w ? L.nnz_d : L.nnz_d + L.nnz_w, nd = (double)nD;
+  const double nzw = use_w ? L.nnz_w : 0.0, nw = use_w ? (double)nW : 0.0;
+  double fl_d = 0, by_d = 0, fl_w = 0, by_w = 0;
+  if (nD > 0) {
+    fl_d = nzd * k * (k + 1) + nzd * 2 * k + nd * (k * k * k / 3.0 + 2 * k * k);
+    by_d = nzd * (4 + s) + nzd * k * s + nd * k * s + (nd + 1) * 8;
+    c->cls_ms[0] += ms_d;
+    c->cls_launches[0] += 1;
+    c->cls_flops[0] += fl_d;
+    c->cls_bytes[0] += by_d;
   }
+  if (nW > 0 && use_w) {
+    // per whitened row with n signals: K (n(n+1)k), n×n Cholesky + solves (n³/3 + 2n²),
+    // Zᵀu and Zᵀc (4nk), unwhitening (2k²); bytes: gathers, x' write, x' read + x write
+    const int mx = max_whitened_ntn(c);
+    for (int64_t r = rb; r < re; ++r) {
+      const double n = (double)(L.h_rowptr[r + 1] - L.h_rowptr[r]);
+      if (((int64_t)std::max(n, 1.0) + 15) / 16 <= mx)
+        fl_w += n * (n + 1) * k + n * n * n / 3.0 + 2 * n * n + 4 * n * k + 2 * k * k;
+    }
+    by_w = nzw * (4 + s) + nzw * k * s + nw * k * s * 3 + nw * 16;
+    c->cls_ms[1] += ms_w;
+    c->cls_launches[1] += 1;
+    c->cls_flops[1] += fl_w;
+    c->cls_bytes[1] += by_w;
+  }
+  c->cls_ms[2] += ms_h;
+  c->cls_launches[2] += 1;
+  c->cls_flops[2] += fl_d + fl_w;
+  c->cls_bytes[2] += by_d + by_w;
+  c->solve_ms += ms_d + ms_w;
+  c->solve_launches += 1;
+  c->solve_flops += fl_d + fl_w;
+  c->solve_bytes += by_d + by_w;
   c->last_side = side;
   if (loss_sum) *loss_sum = *c->hsum;
   return 0;
@@ -816,8 +987,12 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
     std::memcpy(&id, id128, 128);
     NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
   }
-  for (auto& sb : c->s)
-    if (!sb.h_rowptr.empty()) set_default_bounds(sb, world, rank);
+  for (int side = 0; side < 2; ++side) {
+    SideBuf& sb = c->s[side];
+    if (sb.h_rowptr.empty()) continue;
+    set_default_bounds(sb, world, rank);
+    if (int rc = build_buckets(c, side)) return rc;
+  }
   return 0;
 }
 
@@ -843,9 +1018,23 @@ int qmfx_solve_kernel_stats(qmfx_ctx* c, double* total_ms, int64_t* launches, do
   return 0;
 }
 
+int qmfx_kernel_stats(qmfx_ctx* c, int cls, double* total_ms, int64_t* launches, double* flops,
+                      double* bytes) {
+  if (cls < 0 || cls > 2) return fail("class must be 0 (direct), 1 (whitened) or 2 (half)");
+  if (total_ms) *total_ms = c->cls_ms[cls];
+  if (launches) *launches = c->cls_launches[cls];
+  if (flops) *flops = c->cls_flops[cls];
+  if (bytes) *bytes = c->cls_bytes[cls];
+  return 0;
+}
+
 int qmfx_reset_stats(qmfx_ctx* c) {
   c->solve_ms = c->solve_flops = c->solve_bytes = 0;
   c->solve_launches = 0;
+  for (int i = 0; i < 3; ++i) {
+    c->cls_ms[i] = c->cls_flops[i] = c->cls_bytes[i] = 0;
+    c->cls_launches[i] = 0;
+  }
   return 0;
 }
 

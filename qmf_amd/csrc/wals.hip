@@ -1,16 +1,26 @@
-// WALS hot path on MI355X (gfx950): fixed-side Gram YᵀY, the fused per-row
-// "Gram + Cholesky + solve" kernel, and the deterministic loss reduction.
+// WALS hot path on MI355X (gfx950).
 //
 // Reference path (taozhijiang/qmf):
-//   WALSEngine::iterate            qmf/wals/WALSEngine.cpp:165-218
-//   WALSEngine::computeXtX         qmf/wals/WALSEngine.cpp:246-264
+//   WALSEngine::iterate             qmf/wals/WALSEngine.cpp:165-218
+//   WALSEngine::computeXtX          qmf/wals/WALSEngine.cpp:246-264
 //   WALSEngine::updateFactorsForOne qmf/wals/WALSEngine.cpp:266-310
-//   linearSymmetricSolve → dsysv_  qmf/Matrix.cpp:81-96
+//   linearSymmetricSolve → dsysv_   qmf/Matrix.cpp:81-96
 //
-// Data layout in HBM: factors are row-major [n][KP] with KP = 16·NT ≥ k (padding columns
-// are zero); a side's interactions are CSR (int64 rowptr, int32 column = index of the
-// other side, value v).  The padded part of each system is the identity, so padded
-// solution entries are exactly zero.
+// Per solved row r with signals e (fixed-side rows y_e, weights w_e = αv_e, c_e = 1 + αv_e):
+//   A = M + Σ_e w_e y_e y_eᵀ,  M = YᵀY + λI,  b = Σ_e c_e y_e,  x = A⁻¹ b,
+//   loss_r = Σc + xᵀ(A − λI)x − 2xᵀb = Σc − xᵀb − λ‖x‖²      (since Ax = b).
+// Two mathematically identical ways to get x, chosen per row by its signal count n:
+//   * direct (n large):  the k×k Gram of the row, then a register-tile Cholesky;
+//   * whitened (n ≤ k/2, n ≤ 64): with M = L Lᵀ and Z = Y L⁻ᵀ (one GEMM per half),
+//       A = L (I + Zₛᵀ W Zₛ) Lᵀ and, by the push-through identity,
+//       x = L⁻ᵀ Zₛᵀ u  with  (W_P⁻¹ + K_PP) u_P = W_P⁻¹ c_P − K_PQ 1_Q,  u_Q = 1,
+//     where K = Zₛ Zₛᵀ (n×n), P = signals with w > 0, Q = signals with w = 0 (c = 1).
+//     The n×n system replaces the k×k one; x' = Zₛᵀu is mapped back by x = L⁻ᵀ x'
+//     (a GEMM over those rows).  xᵀb = x'ᵀ(Zₛᵀc).
+//
+// Data layout in HBM: factors row-major [n][KP], KP = 16·NT ≥ k, zero padding columns;
+// interactions CSR (int64 rowptr, int32 column, value v).  The padded part of every system
+// is the identity, so padded solution entries are exactly zero.
 #include "common.h"
 #include "kernels.h"
 
@@ -18,36 +28,218 @@ namespace qmfx {
 
 __host__ __device__ constexpr int tile_index(int I, int J) { return I * (I + 1) / 2 + J; }
 
+// Square root / reciprocal inside the factorizations.  fp32: hardware v_sqrt_f32 /
+// v_rcp_f32 (1 ulp; the IEEE-exact expansions cost ~27 instructions each, on the critical
+// path twice per column).  fp64: correctly rounded (the tight-parity path).
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
+
+// Sum over the 16 lanes of a DPP row (lanes 16g..16g+15); every lane receives the sum.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+  return v;
+}
+template <int CTL>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_mov_f64<0x128>(v);
+  v += dpp_mov_f64<0x124>(v);
+  v += dpp_mov_f64<0x122>(v);
+  v += dpp_mov_f64<0x121>(v);
+  return v;
+}
+
 // ---------------------------------------------------------------------------------------
-// Fused row solve.  One wave64 per row; the row's k×k system never leaves the chip.
-//   1. Gram: A = G + Σ_e αv_e y_e y_eᵀ accumulated by 16x16x4 MFMAs straight into the
-//      lower-triangle tiles held in accumulator registers (all NT(NT+1)/2 tiles), the
-//      right-hand side b = Σ (1+αv) y and Σ(1+αv) on the side.
-//   2. Right-looking blocked Cholesky over 16-column panels.  A panel is factored with its
-//      rows spread over the lanes (right-looking column steps, broadcasts by readlane);
-//      the forward solve L y = b rides along as one more register per row, and 16 identity
-//      rows appended to the panel yield L(p,p)⁻ᵀ in the same pass.  The trailing update
-//      A(I,J) −= L(I,p) L(J,p)ᵀ is 4 MFMAs per tile, operands staged through LDS.
-//   3. Backward solve Lᵀ x = y by 16-blocks using the L tiles left in registers and the
-//      L(p,p)⁻ᵀ tiles kept in LDS.
-//   4. loss_row = Σc − xᵀb − λ‖x‖²  (= Σc + xᵀBx − 2xᵀb since (B+λI)x = b; B = A − λI).
+// Register-tile Cholesky + solve, shared by both row kernels (one wave64 per system).
+//   In:  acc = lower 16×16 tiles of an SPD matrix of size 16·NT (diagonal tiles full);
+//        S.bw = right-hand side (written and synchronised by the caller).
+//   Out: S.xs = solution; S.bw = L⁻¹ b.  `bad` set on a non-positive pivot.
+// Right-looking over 16-column panels: a panel is factored with its rows spread over the
+// lanes (column steps broadcast by readlane), the forward solve riding along as one more
+// register per row; the trailing update A(I,J) −= L(I,p)L(J,p)ᵀ is 4 MFMAs per tile with
+// operands staged through LDS; off-diagonal L tiles return to the registers, diagonal
+// ones to LDS.  Backward solve by 16-blocks: off-diagonal part from the register tiles
+// with a cross-lane reduction, the diagonal triangle by a 16-step substitution with the
+// tile's columns in lanes.
 // ---------------------------------------------------------------------------------------
 template <typename T, int NT>
-__global__ __launch_bounds__(64, 2) void wals_solve_kernel(SolveArgs<T> a) {
+struct CholShared {
+  T panel[16 * NT * 17];
+  T Ldiag[NT * 16 * 17];
+  T bw[16 * NT];
+  T xs[16 * NT];
+  T invd[16 * NT];
+};
+
+template <typename T, int NT>
+__device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
+                                           CholShared<T, NT>& S, int lane, int& bad,
+                                           int ablate) {
+  using M = Mfma<T>;
+  constexpr int KP = 16 * NT;
+  constexpr int SLOTS = (KP + 63) / 64;
+  constexpr int PLD = 17;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  for (int p = 0; p < NT; ++p) {
+    const int R = KP - 16 * p;
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        if (J == p) {
+          const int t = tile_index(I, J);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[t][r];
+        }
+      }
+    }
+    __syncthreads();
+    T pa[SLOTS][16];
+    T pb[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int q = lane + 64 * s;
+      const int qq = q < R ? q : 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) pa[s][c] = S.panel[qq * PLD + c];
+      pb[s] = S.bw[16 * p + qq];
+    }
+    if (!(ablate & 2)) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const T d = readlane(pa[0][c], c);
+        bad |= !(d > T(0));
+        const T ljj = fast_sqrt(d);
+        const T inv = fast_rcp(ljj);
+        if (lane == 0) S.invd[16 * p + c] = inv;
+        // lq = L[q][c] below the diagonal, 0 elsewhere: the updates are unconditional FMAs
+        T lq[SLOTS];
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s) {
+          lq[s] = T(0);
+          if (64 * s < R) {
+            const int q = lane + 64 * s;
+            lq[s] = q > c ? pa[s][c] * inv : T(0);
+            pa[s][c] = q > c ? lq[s] : (q == c ? ljj : pa[s][c]);
+          }
+        }
+        const T yc = readlane(pb[0], c) * inv;
+        if (lane == 0) S.bw[16 * p + c] = yc;
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s)
+          if (64 * s < R) pb[s] -= lq[s] * yc;
+#pragma unroll
+        for (int m = c + 1; m < 16; ++m) {
+          const T lm = readlane(lq[0], m);
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s)
+            if (64 * s < R) pa[s][m] -= lq[s] * lm;
+        }
+        // one column per scheduling window: hoisting readlanes across columns blows the
+        // SGPR budget
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int q = lane + 64 * s;
+      if (q < R) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[s][c];
+      }
+      if (q >= 16 && q < R) S.bw[16 * p + q] = pb[s];
+    }
+    __syncthreads();
+    for (int idx = lane; idx < 256; idx += 64) {
+      const int r = idx >> 4, c = idx & 15;
+      S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
+    }
+    T fr[NT][4];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+      if (I > p) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fr[I][s] = S.panel[(16 * (I - p) + cl) * PLD + 4 * s + kk];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fr[I][s] = T(0);
+      }
+    }
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        if (J == p && I > p) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[t][r] = S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
+        } else if (J > p && !(ablate & 4)) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[t] = M::mma(-fr[I][s], fr[J][s], acc[t]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // backward solve Lᵀ x = y
+#pragma unroll
+  for (int I = NT - 1; I >= 0; --I) {
+    if (ablate & 8) break;
+    T part = T(0);
+#pragma unroll
+    for (int J = I + 1; J < NT; ++J) {
+      const int t = tile_index(J, I);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part += acc[t][r] * S.xs[16 * J + M::crow(lane, r)];
+    }
+    part += shfl_xor(part, 16);
+    part += shfl_xor(part, 32);
+    // lane (cl) holds v[cl] and column cl of L(I,I): lc[c] = L[c][cl]
+    T vm = S.bw[16 * I + cl] - part;
+    T lc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lc[c] = S.Ldiag[(I * 16 + c) * PLD + cl];
+#pragma unroll
+    for (int c = 15; c >= 0; --c) {
+      const T xc = readlane(vm, c) * S.invd[16 * I + c];
+      if (lane == 0) S.xs[16 * I + c] = xc;
+      if (cl < c) vm -= lc[c] * xc;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Direct row kernel: one wave64 per row.  Gram A = G + λI + Σ w y yᵀ by 16x16x4 MFMAs into
+// the lower tiles held in registers; b = Σ c y and Σc on the side.  A row's (col, v) pairs
+// are fetched 64 at a time with one coalesced load and broadcast per 4-signal step; the
+// gathers of step s+1 are in flight while the MFMAs of step s run.
+// ---------------------------------------------------------------------------------------
+#ifndef QMFX_WAVES_NT8
+#define QMFX_WAVES_NT8 2
+#endif
+template <typename T, int NT>
+__global__ __launch_bounds__(64, (NT >= 8 && sizeof(T) == 4) ? QMFX_WAVES_NT8 : 2)
+void wals_direct_kernel(SolveArgs<T> a) {
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   constexpr int KP = 16 * NT;
   constexpr int NTT = NT * (NT + 1) / 2;
-  constexpr int PR = KP + 16;  // panel rows at p = 0, identity rows included
-  constexpr int SLOTS = (PR + 63) / 64;
-  constexpr int PLD = 17;
-  __shared__ __attribute__((aligned(16))) T lds[PR * PLD + NT * 16 * PLD + 3 * KP + 16];
-  T* panel = lds;
-  T* Xinv = panel + PR * PLD;
-  T* borig = Xinv + NT * 16 * PLD;
-  T* bw = borig + KP;
-  T* xs = bw + KP;
-  T* vtmp = xs + KP;
+  __shared__ __attribute__((aligned(16))) CholShared<T, NT> S;
+  __shared__ __attribute__((aligned(16))) T borig[KP];
 
   const int lane = threadIdx.x;
   const int cl = lane & 15;
@@ -57,7 +249,6 @@ __global__ __launch_bounds__(64, 2) void wals_solve_kernel(SolveArgs<T> a) {
   const int64_t beg = a.rowptr[row];
   const int64_t end = a.rowptr[row + 1];
 
-  // ---- 1. Gram ------------------------------------------------------------------------
   acc_t acc[NTT];
 #pragma unroll
   for (int I = 0; I < NT; ++I) {
@@ -77,29 +268,44 @@ __global__ __launch_bounds__(64, 2) void wals_solve_kernel(SolveArgs<T> a) {
 #pragma unroll
   for (int c = 0; c < NT; ++c) bpart[c] = T(0);
   double csum = 0.0;
-  for (int64_t e0 = beg; e0 < end; e0 += 4) {
-    const int64_t e = e0 + kk;
-    const bool valid = e < end;
-    const int64_t ec = valid ? e : beg;
-    const int c = a.col[ec];
-    const T v = a.val[ec];
-    const T w = valid ? a.alpha * v : T(0);
-    const T cw = valid ? T(1) + a.alpha * v : T(0);
-    const T* yrow = a.Y + (int64_t)c * KP + cl;
-    T yv[NT], wy[NT];
+  for (int64_t base = beg; base < end && !(a.ablate & 1); base += 64) {
+    const int nst = (int)(end - base < 64 ? end - base : 64);
+    const int cr = lane < nst ? a.col[base + lane] : 0;
+    const T vr = lane < nst ? a.val[base + lane] : T(0);
+    bool valid = kk < nst;
+    T v = __shfl(vr, kk, 64);
+    T yn[NT];
+    {
+      const T* yrow = a.Y + (int64_t)__shfl(cr, kk, 64) * KP + cl;
 #pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      yv[q] = valid ? yrow[16 * q] : T(0);
-      wy[q] = w * yv[q];
-      bpart[q] += cw * yv[q];
+      for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
     }
-    csum += (double)cw;
+    for (int s = 0; 4 * s < nst; ++s) {
+      T yv[NT];
 #pragma unroll
-    for (int I = 0; I < NT; ++I) {
+      for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
+      const T w = valid ? a.alpha * v : T(0);
+      const T cw = valid ? T(1) + a.alpha * v : T(0);
+      const int jn = 4 * (s + 1) + kk;
+      const bool vn = jn < nst;
+      if (4 * (s + 1) < nst) {
+        const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
+        v = __shfl(vr, jn < 64 ? jn : 0, 64);
+        const T* yrow = a.Y + (int64_t)(vn ? cn : cr) * KP + cl;
 #pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const int t = tile_index(I, J);
-        acc[t] = M::mma(yv[I], wy[J], acc[t]);
+        for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
+      }
+      valid = vn;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
+      csum += (double)cw;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+          acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+        }
       }
     }
   }
@@ -109,143 +315,17 @@ __global__ __launch_bounds__(64, 2) void wals_solve_kernel(SolveArgs<T> a) {
     bpart[q] += shfl_xor(bpart[q], 32);
     if (kk == 0) {
       borig[16 * q + cl] = bpart[q];
-      bw[16 * q + cl] = bpart[q];
+      S.bw[16 * q + cl] = bpart[q];
     }
   }
   csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
   int bad = 0;
   __syncthreads();
+  chol_solve<T, NT>(acc, S, lane, bad, a.ablate);
 
-  // ---- 2. blocked Cholesky + forward solve -------------------------------------------
-  for (int p = 0; p < NT; ++p) {
-    const int R = KP - 16 * p;
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-#pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        if (J == p) {
-          const int t = tile_index(I, J);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[t][r];
-        }
-      }
-    }
-    __syncthreads();
-    T pa[SLOTS][16];
-    T pb[SLOTS];
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      const int q = lane + 64 * s;
-      if (q < R) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) pa[s][c] = panel[q * PLD + c];
-        pb[s] = bw[16 * p + q];
-      } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) pa[s][c] = (q - R == c) ? T(1) : T(0);
-        pb[s] = T(0);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const T d = readlane(pa[0][c], c);
-      bad |= !(d > T(0));
-      const T ljj = sqrt(d);
-      const T inv = T(1) / ljj;
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        const int q = lane + 64 * s;
-        if (q > c) pa[s][c] *= inv;
-        else if (q == c) pa[s][c] = ljj;
-      }
-      const T yc = readlane(pb[0], c) * inv;
-      if (lane == 0) bw[16 * p + c] = yc;
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        const int q = lane + 64 * s;
-        if (q > c) pb[s] -= pa[s][c] * yc;
-      }
-#pragma unroll
-      for (int m = c + 1; m < 16; ++m) {
-        const T lm = readlane(pa[0][c], m);
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          const int q = lane + 64 * s;
-          if (q > c) pa[s][m] -= pa[s][c] * lm;
-        }
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      const int q = lane + 64 * s;
-      if (q < R + 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) panel[q * PLD + c] = pa[s][c];
-      }
-      if (q >= 16 && q < R) bw[16 * p + q] = pb[s];
-    }
-    __syncthreads();
-    for (int idx = lane; idx < 256; idx += 64) {
-      const int r = idx >> 4, c = idx & 15;
-      Xinv[(p * 16 + r) * PLD + c] = panel[(R + r) * PLD + c];
-    }
-    T fr[NT][4];
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-      if (I > p) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) fr[I][s] = panel[(16 * (I - p) + cl) * PLD + 4 * s + kk];
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) fr[I][s] = T(0);
-      }
-    }
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-#pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const int t = tile_index(I, J);
-        if (J == p && I > p) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc[t][r] = panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
-        } else if (J > p) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc[t] = M::mma(-fr[I][s], fr[J][s], acc[t]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- 3. backward solve Lᵀ x = y -------------------------------------------------------
-#pragma unroll
-  for (int I = NT - 1; I >= 0; --I) {
-    T part = T(0);
-#pragma unroll
-    for (int J = I + 1; J < NT; ++J) {
-      const int t = tile_index(J, I);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part += acc[t][r] * xs[16 * J + M::crow(lane, r)];
-    }
-    part += shfl_xor(part, 16);
-    part += shfl_xor(part, 32);
-    if (kk == 0) vtmp[cl] = bw[16 * I + cl] - part;
-    __syncthreads();
-    if (lane < 16) {
-      T s = T(0);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) s += Xinv[(I * 16 + lane) * PLD + j] * vtmp[j];
-      xs[16 * I + lane] = s;
-    }
-    __syncthreads();
-  }
-
-  // ---- 4. loss + store ----------------------------------------------------------------
   double xb = 0.0, xx = 0.0;
   for (int i = lane; i < KP; i += 64) {
-    const T xi = xs[i];
+    const T xi = S.xs[i];
     a.X[row * KP + i] = xi;
     xb += (double)xi * (double)borig[i];
     xx += (double)xi * (double)xi;
@@ -259,8 +339,305 @@ __global__ __launch_bounds__(64, 2) void wals_solve_kernel(SolveArgs<T> a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Whitened row kernel (n ≤ 16·NTN signals, n ≤ KP/2).  One wave64 per row.  The row's
+// whitened fixed-side rows z_e (KP values each) are loaded ONCE into registers in MFMA
+// operand order (lane (i, g) holds z_{16I+i}[16q + 4g .. +3] for every I, q), so that
+//   K = Zₛ Zₛᵀ         — NTN(NTN+1)/2 tiles × KP/4 steps of 16x16x4 MFMA from registers,
+//   x' = Zₛᵀu, Zₛᵀc   — per-lane FMAs + 16-lane DPP row sums,
+// and the HBM traffic per signal is one gathered row, as in the direct kernel.
+// Writes x' (whitened); whiten_kernel<UNWHITEN> maps it to x = L⁻ᵀ x' and adds −λ‖x‖².
+// ---------------------------------------------------------------------------------------
+template <typename T, int NTK, int NTN>
+__global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  using v4 = typename M::acc_t;  // 4-wide vector of T
+  constexpr int KP = 16 * NTK;
+  constexpr int NTT = NTN * (NTN + 1) / 2;
+  __shared__ __attribute__((aligned(16))) CholShared<T, NTN> S;
+  __shared__ __attribute__((aligned(16))) T gq[16 * NTN];
+
+  const int lane = threadIdx.x;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const int64_t slot = a.row_begin + blockIdx.x;
+  const int64_t row = a.order ? a.order[slot] : slot;
+  const int64_t beg = a.rowptr[row];
+  const int n = (int)(a.rowptr[row + 1] - beg);  // ≤ 16·NTN by bucketing
+
+  // signal e = lane: column, weight, confidence
+  const bool mine = lane < n;
+  const int cr = mine ? a.col[beg + lane] : 0;
+  const T vr = mine ? a.val[beg + lane] : T(0);
+  const T wl = mine ? a.alpha * vr : T(0);
+  const T cwl = mine ? T(1) + a.alpha * vr : T(0);
+  const bool isP = mine && wl > T(0);
+  const bool isQ = mine && wl == T(0);
+  int bad = __any(mine && wl < T(0)) ? 1 : 0;  // negative confidence: not SPD in this form
+  const bool hasQ = __any(isQ);
+
+  // gather Zₛ into registers: zr[I][q] = z_{16I+cl}[16q + 4kk .. +3]
+  v4 zr[NTN][NTK];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int e = 16 * I + cl;
+    const int ce = __shfl(cr, e, 64);
+    const bool ve = e < n;
+    const v4* zrow = reinterpret_cast<const v4*>(a.Y + (int64_t)ce * KP) + kk;
+#pragma unroll
+    for (int q = 0; q < NTK; ++q) {
+      const v4 z = zrow[4 * q];
+      zr[I][q] = ve ? z : v4{0, 0, 0, 0};
+    }
+  }
+  // K = Zₛ Zₛᵀ (lower tiles); the summation index j = 16q + 4kk + comp is the same for the
+  // A and B operands, so its order within a step does not matter
+  acc_t acc[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < NTK; ++q) {
+#pragma unroll
+    for (int comp = 0; comp < 4; ++comp) {
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+          acc[t] = M::mma(zr[I][q][comp], zr[J][q][comp], acc[t]);
+        }
+      }
+    }
+  }
+  // right-hand side W_P⁻¹ c_P − K_PQ 1_Q  (kq_e = z_eᵀ Σ_{f∈Q} z_f)
+  T rhs = isP ? cwl * fast_rcp(wl) : T(0);
+  if (hasQ) {
+    T gpart[NTK][4];
+#pragma unroll
+    for (int q = 0; q < NTK; ++q)
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = T(0);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const bool qe = __shfl((int)isQ, 16 * I + cl, 64) != 0;
+#pragma unroll
+      for (int q = 0; q < NTK; ++q)
+#pragma unroll
+        for (int comp = 0; comp < 4; ++comp)
+          if (qe) gpart[q][comp] += zr[I][q][comp];
+    }
+#pragma unroll
+    for (int q = 0; q < NTK; ++q)
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = row16_sum(gpart[q][comp]);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      T s = T(0);
+#pragma unroll
+      for (int q = 0; q < NTK; ++q)
+#pragma unroll
+        for (int comp = 0; comp < 4; ++comp) s += zr[I][q][comp] * gpart[q][comp];
+      s += shfl_xor(s, 16);
+      s += shfl_xor(s, 32);
+      if (kk == 0) gq[16 * I + cl] = s;
+    }
+    __syncthreads();
+    const T kqv = lane < 16 * NTN ? gq[lane] : T(0);
+    if (isP) rhs -= kqv;
+  }
+  // S = W_P⁻¹ + K_PP on P×P, identity elsewhere (Q rows and padding)
+  const T iw = isP ? fast_rcp(wl) : T(0);
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const int t = tile_index(I, J);
+      const int f = 16 * J + cl;
+      const bool pf = __shfl((int)isP, f, 64) != 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = 16 * I + M::crow(lane, r);
+        const bool pe = __shfl((int)isP, e, 64) != 0;
+        const T iwe = __shfl(iw, e, 64);
+        T v = acc[t][r];
+        if (pe && pf) v += (e == f) ? iwe : T(0);
+        else v = (e == f) ? T(1) : T(0);
+        acc[t][r] = v;
+      }
+    }
+  }
+  if (lane < 16 * NTN) S.bw[lane] = rhs;
+  __syncthreads();
+  chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
+  // u_e: solved for P, 1 for Q (c = 1), 0 for padding
+  T ul[NTN], cv[NTN];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int e = 16 * I + cl;
+    const bool pe = __shfl((int)isP, e, 64) != 0;
+    const bool qe = __shfl((int)isQ, e, 64) != 0;
+    ul[I] = pe ? S.xs[e] : (qe ? T(1) : T(0));
+    cv[I] = __shfl(cwl, e, 64);
+  }
+  // x' = Zₛᵀ u and b' = Zₛᵀ c, column j = 16q + 4kk + comp
+  T xp[NTK][4];
+  double xb = 0.0;
+#pragma unroll
+  for (int q = 0; q < NTK; ++q) {
+#pragma unroll
+    for (int comp = 0; comp < 4; ++comp) {
+      T sx = T(0), sb = T(0);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        sx += zr[I][q][comp] * ul[I];
+        sb += zr[I][q][comp] * cv[I];
+      }
+      xp[q][comp] = row16_sum(sx);
+      xb += (double)xp[q][comp] * (double)row16_sum(sb);
+    }
+  }
+  // store x' (lane cl == q of each group writes its 4 columns)
+#pragma unroll
+  for (int q = 0; q < NTK; ++q) {
+    if (cl == q) {
+      v4 o = {xp[q][0], xp[q][1], xp[q][2], xp[q][3]};
+      reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
+    }
+  }
+  xb = wave_sum(cl == 0 ? xb : 0.0);
+  const double csum = wave_sum((double)cwl);
+  if (lane == 0) {
+    a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
+    if (bad && a.status) a.status[row] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Whitening / unwhitening GEMMs with the inverse Cholesky factor Linv = L⁻¹ (lower, KP×KP).
+//   whiten:   Z[r] = Linv · Y[r]     (z = L⁻¹ y)            rows 0..n-1, 16 per wave
+//   unwhiten: X[r] = Linvᵀ · X'[r]   (x = L⁻ᵀ x') in place, rows from `order`; also
+//             rowloss[r] −= λ‖x‖².
+// One wave computes a 16-row × KP block with NT accumulator tiles; the zero upper
+// triangle of Linv is skipped.
+// ---------------------------------------------------------------------------------------
+template <typename T, int NT, bool UNWHITEN>
+__global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const int64_t* order,
+                                                     int64_t nrows, const T* __restrict__ Linv,
+                                                     double* rowloss, double lambda) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  constexpr int KP = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (r0 >= nrows) return;
+  const int64_t ra = r0 + cl < nrows ? r0 + cl : nrows - 1;
+  const int64_t rowa = UNWHITEN ? order[ra] : ra;
+  acc_t acc[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) acc[J] = acc_t{0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < KP / 4; ++s) {
+    const int m = 4 * s + kk;
+    const T av = in[rowa * KP + m];
+#pragma unroll
+    for (int J = 0; J < NT; ++J) {
+      const int j = 16 * J + cl;
+      if (UNWHITEN) {
+        // x_j = Σ_m x'_m Linv[m][j]: nonzero only for m ≥ j
+        if (4 * s + 3 >= 16 * J) acc[J] = M::mma(av, Linv[m * KP + j], acc[J]);
+      } else {
+        // z_j = Σ_m Linv[j][m] y_m: nonzero only for m ≤ j
+        if (4 * s <= 16 * J + 15) acc[J] = M::mma(av, Linv[j * KP + m], acc[J]);
+      }
+    }
+  }
+  // all reads of this wave's rows are done before any write (in-place unwhitening)
+  T ss[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t ro = r0 + M::crow(lane, r);
+    if (ro < nrows) {
+      const int64_t rowo = UNWHITEN ? order[ro] : ro;
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+        out[rowo * KP + 16 * J + cl] = acc[J][r];
+        ss[r] += acc[J][r] * acc[J][r];
+      }
+    }
+  }
+  if (UNWHITEN) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const T tot = row16_sum(ss[r]);
+      const int64_t ro = r0 + M::crow(lane, r);
+      if (cl == 0 && ro < nrows) rowloss[order[ro]] -= lambda * (double)tot;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// M = G + λI (padding: 1) → L (Cholesky, fp64, in LDS) → Linv = L⁻¹ written in T.
+// One 256-thread workgroup; run once per half when whitened rows exist.
+// ---------------------------------------------------------------------------------------
+template <typename T, int NT>
+__global__ __launch_bounds__(256) void chol_inv_kernel(const T* G, int k, double lambda,
+                                                       T* Linv, int32_t* status) {
+  constexpr int KP = 16 * NT;
+  constexpr int LD = KP + 1;
+  __shared__ double A[KP * LD];
+  __shared__ double dinv[KP];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < KP * KP; idx += 256) {
+    const int i = idx / KP, j = idx % KP;
+    double v = (double)G[idx];
+    if (i == j) v += i < k ? lambda : 1.0;
+    A[i * LD + j] = v;
+  }
+  __syncthreads();
+  for (int j = 0; j < KP; ++j) {
+    if (tid == 0) {
+      const double d = A[j * LD + j];
+      if (!(d > 0.0)) *status = 1;
+      const double l = sqrt(d > 0.0 ? d : 1.0);
+      A[j * LD + j] = l;
+      dinv[j] = 1.0 / l;
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < KP; i += 256) A[i * LD + j] *= dinv[j];
+    __syncthreads();
+    const int m = KP - j - 1;  // trailing size
+    for (int idx = tid; idx < m * m; idx += 256) {
+      const int ii = j + 1 + idx / m, mm = j + 1 + idx % m;
+      if (mm <= ii) A[ii * LD + mm] -= A[ii * LD + j] * A[mm * LD + j];
+    }
+    __syncthreads();
+  }
+  // Linv column c (thread c): Linv[c][c] = 1/L[c][c];
+  // Linv[i][c] = −(Σ_{m=c}^{i−1} L[i][m] Linv[m][c]) / L[i][i], kept in A's upper triangle
+  // at A[c][i] (row c is private to thread c)
+  if (tid < KP) {
+    const int c = tid;
+    for (int i = c + 1; i < KP; ++i) {
+      double s = A[i * LD + c] * dinv[c];
+      for (int m = c + 1; m < i; ++m) s += A[i * LD + m] * A[c * LD + m];
+      A[c * LD + i] = -s * dinv[i];
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < KP * KP; idx += 256) {
+    const int i = idx / KP, c = idx % KP;
+    double v = 0.0;
+    if (i == c) v = dinv[c];
+    else if (i > c) v = A[c * LD + i];
+    Linv[idx] = (T)v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // YᵀY (WALSEngine.cpp:246-264, without its OpenMP race): each wave accumulates a block of
-// rows into all lower tiles with MFMA, writes its partial; a second kernel adds the
+// rows into all lower tiles with MFMA and writes its partial; a second kernel adds the
 // partials in fixed order (deterministic) in fp64 and mirrors the upper triangle.
 // ---------------------------------------------------------------------------------------
 template <typename T, int NT>
@@ -318,8 +695,7 @@ __global__ void gram_reduce_kernel(const double* partial, int nblocks, T* G) {
   G[idx] = (T)s;
 }
 
-// Fixed-order sum of the per-row losses (ParallelExecutor's fold order is replaced by a
-// deterministic tree; the value is a reporting quantity only).
+// Fixed-order sum of the per-row losses (the value is a reporting quantity only).
 __global__ void sum_f64_kernel(const double* x, int64_t n, double* out) {
   __shared__ double red[256];
   double s = 0.0;
@@ -347,9 +723,52 @@ __global__ void mfma_selftest_kernel(const T* A, const T* B, T* C) {
 // Host launchers.
 // ---------------------------------------------------------------------------------------
 template <typename T, int NT>
-static hipError_t launch_solve_nt(const SolveArgs<T>& a, hipStream_t s) {
+static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
-  hipLaunchKernelGGL((wals_solve_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int NTK>
+static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
+  if (a.nrows <= 0) return hipSuccess;
+  const dim3 g((unsigned)a.nrows), b(64);
+  if (ntn == 1) {
+    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 1>), g, b, 0, s, a);
+  } else if (ntn == 2) {
+    if constexpr (NTK >= 4) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 2>), g, b, 0, s, a);
+    else return hipErrorInvalidValue;
+  } else if (ntn == 3) {
+    if constexpr (NTK >= 6) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 3>), g, b, 0, s, a);
+    else return hipErrorInvalidValue;
+  } else if (ntn == 4) {
+    if constexpr (NTK >= 8) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 4>), g, b, 0, s, a);
+    else return hipErrorInvalidValue;
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename T, int NT>
+static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, int64_t nrows,
+                                   const T* Linv, double* rowloss, double lambda, bool unwhiten,
+                                   hipStream_t s) {
+  if (nrows <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((nrows + 63) / 64);
+  if (unwhiten)
+    hipLaunchKernelGGL((whiten_kernel<T, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, order,
+                       nrows, Linv, rowloss, lambda);
+  else
+    hipLaunchKernelGGL((whiten_kernel<T, NT, false>), dim3(blocks), dim3(256), 0, s, in, out,
+                       order, nrows, Linv, rowloss, lambda);
+  return hipGetLastError();
+}
+
+template <typename T, int NT>
+static hipError_t launch_chol_inv_nt(const T* G, int k, double lambda, T* Linv, int32_t* status,
+                                     hipStream_t s) {
+  hipLaunchKernelGGL((chol_inv_kernel<T, NT>), dim3(1), dim3(256), 0, s, G, k, lambda, Linv, status);
   return hipGetLastError();
 }
 
@@ -370,54 +789,83 @@ static hipError_t launch_gram_nt(const T* Y, int64_t n, T* G, double* partial,
   return hipGetLastError();
 }
 
-#define QMFX_NT_SWITCH(NTV, CALL)                   \
-  switch (NTV) {                                    \
-    case 1: return CALL(1);                         \
-    case 2: return CALL(2);                         \
-    case 3: return CALL(3);                         \
-    case 4: return CALL(4);                         \
-    case 5: return CALL(5);                         \
-    case 6: return CALL(6);                         \
-    case 7: return CALL(7);                         \
-    case 8: return CALL(8);                         \
-    default: return hipErrorInvalidValue;           \
+#define QMFX_NT_SWITCH(NTV, CALL)         \
+  switch (NTV) {                          \
+    case 1: return CALL(1);               \
+    case 2: return CALL(2);               \
+    case 3: return CALL(3);               \
+    case 4: return CALL(4);               \
+    case 5: return CALL(5);               \
+    case 6: return CALL(6);               \
+    case 7: return CALL(7);               \
+    case 8: return CALL(8);               \
+    default: return hipErrorInvalidValue; \
+  }
+#define QMFX_NT_SWITCH64(NTV, CALL)       \
+  switch (NTV) {                          \
+    case 1: return CALL(1);               \
+    case 2: return CALL(2);               \
+    case 3: return CALL(3);               \
+    case 4: return CALL(4);               \
+    default: return hipErrorInvalidValue; \
   }
 
-hipError_t launch_wals_solve_f32(const SolveArgs<float>& a, int nt, hipStream_t s) {
-#define CALL(N) launch_solve_nt<float, N>(a, s)
+hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s) {
+#define CALL(N) launch_direct_nt<float, N>(a, s)
   QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
-
-hipError_t launch_wals_solve_f64(const SolveArgs<double>& a, int nt, hipStream_t s) {
-#define CALL(N) launch_solve_nt<double, N>(a, s)
-  switch (nt) {
-    case 1: return CALL(1);
-    case 2: return CALL(2);
-    case 3: return CALL(3);
-    case 4: return CALL(4);
-    default: return hipErrorInvalidValue;
-  }
+hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s) {
+#define CALL(N) launch_direct_nt<double, N>(a, s)
+  QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
 }
-
-hipError_t launch_gram_f32(const float* Y, int64_t n, int nt, float* G, double* partial,
-                           int max_blocks, hipStream_t s) {
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {
+#define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, s)
+  QMFX_NT_SWITCH(nt, CALL)
+#undef CALL
+}
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
+#define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, s)
+  QMFX_NT_SWITCH64(nt, CALL)
+#undef CALL
+}
+hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,
+                         int nt, const float* Linv, double* rowloss, double lambda,
+                         bool unwhiten, hipStream_t s) {
+#define CALL(N) launch_whiten_nt<float, N>(in, out, order, nrows, Linv, rowloss, lambda, unwhiten, s)
+  QMFX_NT_SWITCH(nt, CALL)
+#undef CALL
+}
+hipError_t launch_whiten(const double* in, double* out, const int64_t* order, int64_t nrows,
+                         int nt, const double* Linv, double* rowloss, double lambda,
+                         bool unwhiten, hipStream_t s) {
+#define CALL(N) launch_whiten_nt<double, N>(in, out, order, nrows, Linv, rowloss, lambda, unwhiten, s)
+  QMFX_NT_SWITCH64(nt, CALL)
+#undef CALL
+}
+hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
+                           int32_t* status, hipStream_t s) {
+#define CALL(N) launch_chol_inv_nt<float, N>(G, k, lambda, Linv, status, s)
+  QMFX_NT_SWITCH(nt, CALL)
+#undef CALL
+}
+hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
+                           int32_t* status, hipStream_t s) {
+#define CALL(N) launch_chol_inv_nt<double, N>(G, k, lambda, Linv, status, s)
+  QMFX_NT_SWITCH64(nt, CALL)
+#undef CALL
+}
+hipError_t launch_gram(const float* Y, int64_t n, int nt, float* G, double* partial,
+                       int max_blocks, hipStream_t s) {
 #define CALL(N) launch_gram_nt<float, N>(Y, n, G, partial, max_blocks, s)
   QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
-
-hipError_t launch_gram_f64(const double* Y, int64_t n, int nt, double* G, double* partial,
-                           int max_blocks, hipStream_t s) {
+hipError_t launch_gram(const double* Y, int64_t n, int nt, double* G, double* partial,
+                       int max_blocks, hipStream_t s) {
 #define CALL(N) launch_gram_nt<double, N>(Y, n, G, partial, max_blocks, s)
-  switch (nt) {
-    case 1: return CALL(1);
-    case 2: return CALL(2);
-    case 3: return CALL(3);
-    case 4: return CALL(4);
-    default: return hipErrorInvalidValue;
-  }
+  QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
 }
 

@@ -145,3 +145,25 @@ def test_indefinite_rows_are_flagged():
     o, c = make_pair(u, i, v, 8, 64, init=np.full((3, 8), 0.3), lam=0.01, alpha=40.0)
     c.wals_half(0, 40.0, 0.01)
     assert 0 in set(c.failed_rows().tolist())
+
+
+@pytest.mark.parametrize("k,precision", [(128, 32), (64, 32), (64, 64), (32, 64)])
+def test_whitened_rows_match_direct_and_oracle(k, precision, monkeypatch):
+    """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
+    QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
+    u, i, v = synth(4000, 900, 30000, seed=11)  # ~7.5 signals per user: whitened users
+    v[::7] = 0.0  # zero-valued signals (Q set: c = 1, w = 0)
+    o, c = make_pair(u, i, v, k, precision, seed=2)
+    monkeypatch.setenv("QMFX_NO_WHITEN", "1")
+    _, cd = make_pair(u, i, v, k, precision, seed=2)
+    monkeypatch.delenv("QMFX_NO_WHITEN")
+    tol = 1e-4 if precision == 32 else 1e-9
+    for side in (0, 1):
+        lo = o.iterate(side)
+        lw = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+        ld = cd.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+        assert rel_err(c.factors(side), o.factors(side)) < tol, side
+        assert rel_err(cd.factors(side), o.factors(side)) < tol, side
+        assert abs(lw - lo) < tol * abs(lo) * 10 and abs(ld - lo) < tol * abs(lo) * 10
+        c.set_factors(side, o.factors(side))
+        cd.set_factors(side, o.factors(side))
