@@ -270,7 +270,7 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipMalloc(&c->G, (size_t)c->kp * c->kp * c->esz);
   if (e == hipSuccess)
     e = hipMalloc(&c->gpart, (size_t)c->gpart_blocks * (nt * (nt + 1) / 2) * 256 * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc(&c->dsum, 4 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->dsum, 1024 * sizeof(double));  // sum + partials
   if (e == hipSuccess) e = hipHostMalloc(&c->hsum, 4 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc(&c->bad, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->eval_partial, 1024 * sizeof(double));

@@ -695,18 +695,30 @@ __global__ void gram_reduce_kernel(const double* partial, int nblocks, T* G) {
   G[idx] = (T)s;
 }
 
-// Fixed-order sum of the per-row losses (the value is a reporting quantity only).
-__global__ void sum_f64_kernel(const double* x, int64_t n, double* out) {
-  __shared__ double red[256];
+// Fixed-order sum of the per-row losses: per-block partials in fixed slots, then one
+// block adds them in order (deterministic; the value is a reporting quantity only).
+constexpr int kSumBlocks = 512;
+__global__ __launch_bounds__(256) void sum_f64_partial_kernel(const double* x, int64_t n,
+                                                              double* partial) {
+  __shared__ double red[4];
+  const int64_t chunk = (n + kSumBlocks - 1) / kSumBlocks;
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = b + chunk < n ? b + chunk : n;
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) s += x[i];
-  red[threadIdx.x] = s;
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *out = red[0];
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ __launch_bounds__(256) void sum_f64_final_kernel(const double* partial, double* out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < kSumBlocks; i += 256) s += partial[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
 }
 
 // MFMA layout self-test: C(16×16) = A(16×4) · B(4×16) written row-major via crow().
@@ -869,8 +881,10 @@ hipError_t launch_gram(const double* Y, int64_t n, int nt, double* G, double* pa
 #undef CALL
 }
 
+// `out` must have room for kSumBlocks + 1 doubles: out[0] = sum, out[1..] = partials.
 hipError_t launch_sum_f64(const double* x, int64_t n, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(sum_f64_kernel, dim3(1), dim3(256), 0, s, x, n, out);
+  hipLaunchKernelGGL(sum_f64_partial_kernel, dim3(kSumBlocks), dim3(256), 0, s, x, n, out + 1);
+  hipLaunchKernelGGL(sum_f64_final_kernel, dim3(1), dim3(256), 0, s, out + 1, out);
   return hipGetLastError();
 }
 
