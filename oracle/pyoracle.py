@@ -72,11 +72,18 @@ def lib():
         L.orc_bpr_loss_sum.restype = ctypes.c_double
         L.orc_bpr_loss_sum.argtypes = [c_f64p, c_f64p, c_f64p, ctypes.c_int, c_i64p,
                                        ctypes.c_int64, ctypes.c_int]
+        L.orc_bpr_sets.restype = ctypes.c_int
+        L.orc_bpr_sets.argtypes = [c_i64p, c_i64p, c_f64p, ctypes.c_int64, c_i64p, c_i64p,
+                                   c_f64p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                   c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p,
+                                   c_i64p]
         _lib = L
     return _lib
 
 
 def _p(a, t):
+    if not a.flags.c_contiguous:
+        raise ValueError("oracle arrays must be C-contiguous")
     return a.ctypes.data_as(t)
 
 
@@ -204,6 +211,8 @@ def update_one(Y, cols, vals, YtY, alpha, lam):
 
 def bpr_update_seq(U, I, bias, triplets, lr, bias_lambda, user_lambda, item_lambda, use_biases):
     """In-place BPREngine::update over triplets (BPREngine.cpp:178-220)."""
+    for a in (U, I, bias):
+        assert a.dtype == np.float64 and a.flags.c_contiguous, "in-place arrays must be C-contiguous f64"
     k = U.shape[1]
     t = np.ascontiguousarray(triplets, np.int64)
     rc = lib().orc_bpr_update_seq(_p(U, c_f64p), _p(I, c_f64p), _p(bias, c_f64p), k,
@@ -214,11 +223,40 @@ def bpr_update_seq(U, I, bias, triplets, lr, bias_lambda, user_lambda, item_lamb
 
 
 def bpr_predict_difference(U, I, bias, u, p, n, use_biases):
+    U, I, bias = (np.ascontiguousarray(a, np.float64) for a in (U, I, bias))
     return lib().orc_bpr_predict_difference(_p(U, c_f64p), _p(I, c_f64p), _p(bias, c_f64p),
                                             U.shape[1], u, p, n, int(use_biases))
 
 
 def bpr_loss_sum(U, I, bias, triplets, use_biases):
+    U, I, bias = (np.ascontiguousarray(a, np.float64) for a in (U, I, bias))
     t = np.ascontiguousarray(triplets, np.int64)
     return lib().orc_bpr_loss_sum(_p(U, c_f64p), _p(I, c_f64p), _p(bias, c_f64p), U.shape[1],
                                   _p(t, c_i64p), len(t), int(use_biases))
+
+
+def bpr_sets(users, items, values, test=None, eval_num_neg=3, eval_seed=42):
+    """BPREngine::init/initTest bookkeeping (BPREngine.cpp:63-131): (uids, iids, evalSet,
+    testEvalSet) with triplets as int64 (n, 3) arrays."""
+    u = np.ascontiguousarray(users, np.int64)
+    i = np.ascontiguousarray(items, np.int64)
+    v = np.ascontiguousarray(values, np.float64)
+    if test is None:
+        test = (np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0))
+    tu = np.ascontiguousarray(test[0], np.int64)
+    ti = np.ascontiguousarray(test[1], np.int64)
+    tv = np.ascontiguousarray(test[2], np.float64)
+    n, tn = len(u), len(tu)
+    nu, ni, ne, nt = (ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64())
+    uids = np.zeros(max(n, 1), np.int64)
+    iids = np.zeros(max(n, 1), np.int64)
+    ev = np.zeros((max(n * eval_num_neg, 1), 3), np.int64)
+    tev = np.zeros((max(tn * eval_num_neg, 1), 3), np.int64)
+    rc = lib().orc_bpr_sets(_p(u, c_i64p), _p(i, c_i64p), _p(v, c_f64p), n, _p(tu, c_i64p),
+                            _p(ti, c_i64p), _p(tv, c_f64p), tn, eval_num_neg, eval_seed,
+                            ctypes.byref(nu), ctypes.byref(ni), _p(uids, c_i64p),
+                            _p(iids, c_i64p), _p(ev, c_i64p), ctypes.byref(ne),
+                            _p(tev, c_i64p), ctypes.byref(nt))
+    if rc:
+        raise ValueError("a user has every item as a positive")
+    return uids[:nu.value], iids[:ni.value], ev[:ne.value], tev[:nt.value]

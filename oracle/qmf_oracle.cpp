@@ -37,7 +37,9 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <random>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include <dlfcn.h>
@@ -632,6 +634,84 @@ double orc_bpr_loss_sum(const double* U, const double* I, const double* bias, in
     s += std::log(1.0 + std::exp(-x));
   }
   return s;
+}
+
+// BPREngine::init (BPREngine.cpp:63-90) and initTest (:92-131) bookkeeping with
+// sampleRandomNegative (BPREngine-inl.h:48-60): first-appearance indexes, value < 1
+// dropped, per-user unordered_set of positives, the evaluation triplets from
+// mt19937(evalSeed) + uniform_int_distribution<int>(0, nitems − 1) with rejection.
+// Outputs: index sizes and ids, eval / test-eval triplets (u, p, n).  Returns 1 (instead
+// of spinning forever like the reference) when some user has every item as a positive.
+int orc_bpr_sets(const int64_t* users, const int64_t* items, const double* vals, int64_t n,
+                 const int64_t* tusers, const int64_t* titems, const double* tvals, int64_t tn,
+                 int64_t evalNumNeg, int32_t evalSeed, int64_t* nusers, int64_t* nitems,
+                 int64_t* uids, int64_t* iids, int64_t* evalSet, int64_t* nEval,
+                 int64_t* testEvalSet, int64_t* nTestEval) {
+  IdIndex ui, ii;
+  std::vector<std::pair<size_t, size_t>> data;
+  for (int64_t e = 0; e < n; ++e) {
+    if (vals[e] < 1.0) continue;
+    const size_t u = ui.getOrSetIdx(users[e]);
+    const size_t p = ii.getOrSetIdx(items[e]);
+    data.emplace_back(u, p);
+  }
+  std::vector<std::unordered_set<size_t>> itemMap(ui.ids.size());
+  for (const auto& d : data) itemMap[d.first].insert(d.second);
+  const size_t ni = ii.ids.size();
+  auto sample = [ni](const std::unordered_set<size_t>& pos, std::mt19937& gen,
+                     size_t* out) -> bool {
+    if (pos.size() >= ni) return false;
+    std::uniform_int_distribution<> dis(0, static_cast<int>(ni) - 1);
+    size_t neg;
+    do {
+      neg = dis(gen);
+    } while (pos.count(neg) > 0);
+    *out = neg;
+    return true;
+  };
+  {
+    std::mt19937 gen(evalSeed);
+    int64_t w = 0;
+    for (const auto& d : data)
+      for (int64_t j = 0; j < evalNumNeg; ++j) {
+        size_t neg;
+        if (!sample(itemMap[d.first], gen, &neg)) return 1;
+        evalSet[3 * w] = (int64_t)d.first;
+        evalSet[3 * w + 1] = (int64_t)d.second;
+        evalSet[3 * w + 2] = (int64_t)neg;
+        ++w;
+      }
+    *nEval = w;
+  }
+  {
+    std::vector<std::unordered_set<size_t>> testMap(ui.ids.size());
+    std::vector<std::pair<size_t, size_t>> valid;
+    for (int64_t e = 0; e < tn; ++e) {
+      if (tvals[e] < 1.0) continue;
+      const size_t u = ui.idx(tusers[e]);
+      const size_t p = ii.idx(titems[e]);
+      if (u == IdIndex::missing || p == IdIndex::missing) continue;
+      testMap[u].insert(p);
+      valid.emplace_back(u, p);
+    }
+    std::mt19937 gen(evalSeed);
+    int64_t w = 0;
+    for (const auto& d : valid)
+      for (int64_t j = 0; j < evalNumNeg; ++j) {
+        size_t neg;
+        if (!sample(testMap[d.first], gen, &neg)) return 1;
+        testEvalSet[3 * w] = (int64_t)d.first;
+        testEvalSet[3 * w + 1] = (int64_t)d.second;
+        testEvalSet[3 * w + 2] = (int64_t)neg;
+        ++w;
+      }
+    *nTestEval = w;
+  }
+  *nusers = (int64_t)ui.ids.size();
+  *nitems = (int64_t)ni;
+  std::copy(ui.ids.begin(), ui.ids.end(), uids);
+  std::copy(ii.ids.begin(), ii.ids.end(), iids);
+  return 0;
 }
 
 }  // extern "C"

@@ -500,7 +500,9 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
 #pragma unroll
   for (int q = 0; q < NTK; ++q) {
     if (cl == q) {
+      // a failed row stores x' = 0 (so x = 0 and its loss term is 0); the host re-solves it
       v4 o = {xp[q][0], xp[q][1], xp[q][2], xp[q][3]};
+      if (bad) o = v4{};
       reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
     }
   }

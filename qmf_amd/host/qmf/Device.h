@@ -1,0 +1,54 @@
+// RAII handle on a qmfx device context (include/qmfx.h) with the reference's error
+// convention: any failing call aborts through LOG(FATAL) with the library's message.
+#pragma once
+
+#include <cstdlib>
+#include <string>
+
+#include <qmfx.h>
+
+#include <qmf/utils/Log.h>
+
+namespace qmf {
+
+// Which GPU and which arithmetic the engines use.  Defaults come from the environment
+// (QMF_DEVICE, QMF_PRECISION), then device 0 and fp32; the CLIs expose --device and
+// --precision.  fp64 matches the reference's Double arithmetic to ~1e-12; fp32 meets the
+// 1e-4 factor tolerance on well-conditioned systems at twice the throughput.
+struct DeviceOptions {
+  int device = envInt("QMF_DEVICE", 0);
+  int precision = envInt("QMF_PRECISION", 32);
+
+  static int envInt(const char* name, int def) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : def;
+  }
+};
+
+#define QMFX_CHECK(call)                                                              \
+  do {                                                                                \
+    const int qmfx_rc_ = (call);                                                      \
+    if (qmfx_rc_ != 0)                                                                \
+      LOG(FATAL) << #call << " failed (" << qmfx_rc_ << "): " << qmfx_last_error();   \
+  } while (0)
+
+class DeviceContext {
+ public:
+  DeviceContext(const DeviceOptions& opt, const size_t nfactors) {
+    CHECK(opt.precision == 32 || opt.precision == 64)
+      << "precision must be 32 or 64, got " << opt.precision;
+    QMFX_CHECK(qmfx_create(&ctx_, opt.device, opt.precision, static_cast<int>(nfactors)));
+  }
+  ~DeviceContext() {
+    if (ctx_) qmfx_destroy(ctx_);
+  }
+  DeviceContext(const DeviceContext&) = delete;
+  DeviceContext& operator=(const DeviceContext&) = delete;
+
+  qmfx_ctx* get() const { return ctx_; }
+
+ private:
+  qmfx_ctx* ctx_ = nullptr;
+};
+
+}  // namespace qmf

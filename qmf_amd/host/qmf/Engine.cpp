@@ -1,0 +1,131 @@
+#include <qmf/Engine.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+#include <random>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+
+#include <qmf/utils/Log.h>
+
+namespace qmf {
+
+void Engine::initAvgTestData(std::vector<size_t>& testUsers,
+                             std::vector<std::vector<Double>>& testLabels,
+                             std::vector<std::vector<Double>>& testScores,
+                             const std::vector<DatasetElem>& testDataset,
+                             const IdIndex& userIndex,
+                             const IdIndex& itemIndex,
+                             const size_t numTestUsers,
+                             const int32_t seed) {
+  // The user order is the iteration order of an unordered_set filled in dataset order,
+  // then (optionally) a mt19937(seed) shuffle: the same containers and calls as the
+  // reference (Engine.cpp:35-52) so the sampled users coincide.
+  std::unordered_set<size_t> seen;
+  for (const auto& e : testDataset) {
+    const size_t u = userIndex.idx(e.userId);
+    const size_t i = itemIndex.idx(e.itemId);
+    if (u != IdIndex::missingIdx && i != IdIndex::missingIdx) seen.insert(u);
+  }
+  testUsers.assign(seen.begin(), seen.end());
+  if (numTestUsers > 0 && numTestUsers < testUsers.size()) {
+    std::shuffle(testUsers.begin(), testUsers.end(), std::mt19937(seed));
+    testUsers.resize(numTestUsers);
+    testUsers.shrink_to_fit();
+  }
+  std::unordered_map<size_t, size_t> slot;
+  testLabels.reserve(testUsers.size());
+  testScores.reserve(testUsers.size());
+  for (size_t t = 0; t < testUsers.size(); ++t) {
+    slot[testUsers[t]] = t;
+    testLabels.emplace_back(itemIndex.size());
+    testScores.emplace_back(itemIndex.size());
+  }
+  for (const auto& e : testDataset) {
+    const size_t u = userIndex.idx(e.userId);
+    const size_t i = itemIndex.idx(e.itemId);
+    if (u == IdIndex::missingIdx || i == IdIndex::missingIdx) continue;
+    const auto it = slot.find(u);
+    if (it != slot.end()) testLabels[it->second][i] = e.value;
+  }
+}
+
+void Engine::computeTestScores(std::vector<std::vector<Double>>& testScores,
+                               const std::vector<size_t>& testUsers,
+                               const FactorData& userFactors,
+                               const FactorData& itemFactors,
+                               ParallelExecutor& parallel) {
+  const size_t k = userFactors.nfactors();
+  const size_t ni = itemFactors.nelems();
+  parallel.execute(testUsers.size(), [&](const size_t t) {
+    const Double* u = userFactors.getFactors().data(testUsers[t]);
+    auto& scores = testScores[t];
+    for (size_t i = 0; i < ni; ++i) {
+      const Double* q = itemFactors.getFactors().data(i);
+      Double s = itemFactors.withBiases() ? itemFactors.biasAt(i) : 0.0;
+      for (size_t f = 0; f < k; ++f) s += u[f] * q[f];
+      scores[i] = s;
+    }
+  });
+}
+
+namespace {
+
+// Formats rows [b, e) exactly as `out << std::fixed << std::setprecision(9)` would:
+// libstdc++ renders fixed doubles through printf("%.*f").
+void formatRows(const FactorData& fd, const IdIndex& index, size_t b, size_t e, std::string& s) {
+  char buf[64];
+  const size_t k = fd.nfactors();
+  for (size_t idx = b; idx < e; ++idx) {
+    int n = std::snprintf(buf, sizeof(buf), "%lld", static_cast<long long>(index.id(idx)));
+    s.append(buf, n);
+    if (fd.withBiases()) {
+      n = std::snprintf(buf, sizeof(buf), " %.9f", fd.biasAt(idx));
+      s.append(buf, n);
+    }
+    const Double* row = fd.getFactors().data(idx);
+    for (size_t f = 0; f < k; ++f) {
+      n = std::snprintf(buf, sizeof(buf), " %.9f", row[f]);
+      if (n < 0 || n >= static_cast<int>(sizeof(buf))) {  // |x| ≥ 1e52: rare, exact path
+        std::string big(static_cast<size_t>(std::snprintf(nullptr, 0, " %.9f", row[f])) + 1, '\0');
+        std::snprintf(&big[0], big.size(), " %.9f", row[f]);
+        big.pop_back();
+        s += big;
+      } else {
+        s.append(buf, n);
+      }
+    }
+    s.push_back('\n');
+  }
+}
+
+}  // namespace
+
+void Engine::saveFactors(const FactorData& factorData, const IdIndex& index,
+                         const std::string& fileName) {
+  std::ofstream fout(fileName);
+  saveFactors(factorData, index, fout);
+}
+
+void Engine::saveFactors(const FactorData& factorData, const IdIndex& index, std::ostream& out) {
+  CHECK_EQ(factorData.nelems(), index.size());
+  const size_t n = factorData.nelems();
+  // format blocks of rows in parallel, write them in order
+  const size_t block = 1 << 14;
+  const size_t nblocks = (n + block - 1) / block;
+  const unsigned hc = std::thread::hardware_concurrency();
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(hc ? hc : 1, 32));
+  for (size_t b0 = 0; b0 < nblocks; b0 += nt) {
+    const size_t nb = std::min(nt, nblocks - b0);
+    std::vector<std::string> parts(nb);
+    ParallelExecutor::run(nb, [&](const size_t t) {
+      const size_t b = (b0 + t) * block;
+      formatRows(factorData, index, b, std::min(n, b + block), parts[t]);
+    });
+    for (const auto& p : parts) out.write(p.data(), static_cast<std::streamsize>(p.size()));
+  }
+}
+
+}  // namespace qmf

@@ -1,0 +1,162 @@
+#include <qmf/wals/WALSEngine.h>
+
+#include <random>
+
+#include <qmf/Matrix.h>
+#include <qmf/utils/Log.h>
+
+namespace qmf {
+
+WALSEngine::WALSEngine(const WALSConfig& config,
+                       const std::unique_ptr<MetricsEngine>& metricsEngine,
+                       const size_t nthreads,
+                       const DeviceOptions& device)
+    : config_(config), metricsEngine_(metricsEngine), deviceOptions_(device),
+      parallel_(nthreads) {
+  if (metricsEngine_ && !metricsEngine_->testAvgMetrics().empty() &&
+      metricsEngine_->config().numTestUsers == 0) {
+    LOG(WARNING) << "computing average test metrics on all users can be slow! "
+                    "Set numTestUsers > 0 to sample some of them";
+  }
+}
+
+WALSEngine::~WALSEngine() = default;
+
+void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
+  CHECK(!userFactors_ && !itemFactors_) << "engine was already initialized with train data";
+  CHECK_GT(config_.nfactors, 0);
+  SignalCsr byUser, byItem;
+  groupSignals(dataset, userIndex_, itemIndex_, byUser, byItem, parallel_.nthreads());
+
+  userFactors_ = std::make_unique<FactorData>(nusers(), config_.nfactors);
+  itemFactors_ = std::make_unique<FactorData>(nitems(), config_.nfactors);
+  if (config_.DistributionFile.empty()) {
+    // not reproducible by design (random_device), as in the reference (WALSEngine.cpp:56-63)
+    std::random_device rd;
+    std::mt19937 gen(rd());
+    std::uniform_real_distribution<Double> distr(-config_.initDistributionBound,
+                                                 config_.initDistributionBound);
+    itemFactors_->setFactors([&](auto...) { return distr(gen); });
+  } else {
+    itemFactors_->setFactors(config_.DistributionFile);
+  }
+
+  dev_ = std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors);
+  qmfx_ctx* c = dev_->get();
+  QMFX_CHECK(qmfx_set_shape(c, static_cast<int64_t>(nusers()), static_cast<int64_t>(nitems())));
+  QMFX_CHECK(qmfx_upload_csr(c, QMFX_USERS, byUser.rowptr.data(), byUser.col.data(),
+                             byUser.val.data(), static_cast<int64_t>(byUser.nnz())));
+  QMFX_CHECK(qmfx_upload_csr(c, QMFX_ITEMS, byItem.rowptr.data(), byItem.col.data(),
+                             byItem.val.data(), static_cast<int64_t>(byItem.nnz())));
+  QMFX_CHECK(qmfx_set_factors(c, QMFX_USERS, userFactors_->getFactors().data()));
+  QMFX_CHECK(qmfx_set_factors(c, QMFX_ITEMS, itemFactors_->getFactors().data()));
+  hostStale_ = false;
+}
+
+void WALSEngine::initTest(const std::vector<DatasetElem>& testDataset) {
+  CHECK(testUsers_.empty()) << "engine was already initialized with test data";
+  if (metricsEngine_ && !metricsEngine_->testAvgMetrics().empty()) {
+    initAvgTestData(testUsers_, testLabels_, testScores_, testDataset, userIndex_, itemIndex_,
+                    metricsEngine_->config().numTestUsers, metricsEngine_->config().seed);
+  }
+}
+
+Double WALSEngine::resolveFailedRows(const int side) {
+  qmfx_ctx* c = dev_->get();
+  int64_t count = 0;
+  QMFX_CHECK(qmfx_wals_failed_rows(c, nullptr, 0, &count));
+  if (count == 0) return 0.0;
+  std::vector<int64_t> rows(static_cast<size_t>(count));
+  QMFX_CHECK(qmfx_wals_failed_rows(c, rows.data(), count, &count));
+  LOG(WARNING) << count << (side == QMFX_USERS ? " user" : " item")
+               << " systems are not positive definite; solving them on the host";
+  const size_t k = config_.nfactors;
+  const Double alpha = config_.confidenceWeight, lambda = config_.regularizationLambda;
+  std::vector<Double> A(k * k), b(k);
+  Double loss = 0.0;
+  for (const int64_t row : rows) {
+    Double csum = 0.0;
+    QMFX_CHECK(qmfx_wals_row_system(c, side, row, alpha, lambda, A.data(), b.data(), &csum));
+    Matrix M(k, k);
+    Vector rhs(k);
+    std::copy(A.begin(), A.end(), M.data());
+    std::copy(b.begin(), b.end(), rhs.data());
+    const Vector x = linearSymmetricSolve(M, rhs);
+    // Σ(1+αv) + xᵀ(A−λI)x − 2xᵀb (WALSEngine.cpp:300-308)
+    Double xAx = 0.0, xb = 0.0, xx = 0.0;
+    for (size_t i = 0; i < k; ++i) {
+      Double ai = 0.0;
+      for (size_t j = 0; j < k; ++j) ai += A[i * k + j] * x(j);
+      xAx += x(i) * ai;
+      xb += x(i) * b[i];
+      xx += x(i) * x(i);
+    }
+    loss += csum + xAx - lambda * xx - 2.0 * xb;
+    QMFX_CHECK(qmfx_wals_set_row(c, side, row, x.data()));
+  }
+  hostResolved_ += rows.size();
+  return loss;
+}
+
+Double WALSEngine::iterate(const int side) {
+  Double sum = 0.0;
+  QMFX_CHECK(qmfx_wals_half(dev_->get(), side, config_.confidenceWeight,
+                            config_.regularizationLambda, &sum));
+  sum += resolveFailedRows(side);
+  hostStale_ = true;
+  lastLoss_ = sum / (static_cast<Double>(nusers()) * static_cast<Double>(nitems()));
+  return lastLoss_;
+}
+
+void WALSEngine::optimize() {
+  CHECK(userFactors_ && itemFactors_) << "no factor data, have you initialized the engine?";
+  for (size_t epoch = 1; epoch <= config_.nepochs; ++epoch) {
+    iterate(QMFX_USERS);                    // item factors fixed
+    const Double loss = iterate(QMFX_ITEMS);  // user factors fixed
+    LOG(INFO) << "epoch " << epoch << ": train loss = " << loss;
+    evaluate(epoch);
+  }
+  QMFX_CHECK(qmfx_sync(dev_->get()));
+}
+
+void WALSEngine::syncHost() const {
+  if (!hostStale_ || !dev_) return;
+  QMFX_CHECK(qmfx_get_factors(dev_->get(), QMFX_USERS, userFactors_->getFactors().data()));
+  QMFX_CHECK(qmfx_get_factors(dev_->get(), QMFX_ITEMS, itemFactors_->getFactors().data()));
+  hostStale_ = false;
+}
+
+void WALSEngine::evaluate(const size_t epoch) {
+  if (metricsEngine_ && !metricsEngine_->testAvgMetrics().empty() && !testUsers_.empty() &&
+      (metricsEngine_->config().alwaysCompute || epoch == config_.nepochs)) {
+    LOG(INFO) << "do compute evaluate ...";
+    syncHost();
+    computeTestScores(testScores_, testUsers_, *userFactors_, *itemFactors_, parallel_);
+    metricsEngine_->computeAndRecordTestAvgMetrics(epoch, testLabels_, testScores_, parallel_);
+  }
+}
+
+const FactorData& WALSEngine::userFactors() const {
+  CHECK(userFactors_) << "user factors wasn't initialized";
+  syncHost();
+  return *userFactors_;
+}
+
+const FactorData& WALSEngine::itemFactors() const {
+  CHECK(itemFactors_) << "item factors wasn't initialized";
+  syncHost();
+  return *itemFactors_;
+}
+
+void WALSEngine::saveUserFactors(const std::string& fileName) const {
+  saveFactors(userFactors(), userIndex_, fileName);
+}
+
+void WALSEngine::saveItemFactors(const std::string& fileName) const {
+  saveFactors(itemFactors(), itemIndex_, fileName);
+}
+
+size_t WALSEngine::nusers() const { return userIndex_.size(); }
+size_t WALSEngine::nitems() const { return itemIndex_.size(); }
+
+}  // namespace qmf

@@ -1,0 +1,210 @@
+"""End-to-end parity of the drop-in CLIs on the MI355X: `wals` / `bpr` (qmf_amd/bin) run
+with the reference's flags, their output files (Engine::saveFactors text) and log lines
+compared with the oracle run on the same inputs.
+
+Tolerances: fp64 1e-9 normwise-relative on factors (the files round to 9 decimals, so
+absolute 5e-10 per entry is the floor); fp32 1e-3 after 10 epochs (per-half 1e-4)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from helpers import ROOT, load_ml100k, load_tiny, rel_err, synth
+
+pytestmark = pytest.mark.gpu
+BIN = os.path.join(ROOT, "qmf_amd", "bin")
+
+
+def run(exe, *flags, timeout=300):
+    r = subprocess.run([os.path.join(BIN, exe)] + list(flags), capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stderr
+
+
+def read_factors(path, biases=False):
+    rows = [line.split(" ") for line in open(path).read().splitlines()]
+    ids = np.array([int(r[0]) for r in rows], np.int64)
+    vals = np.array([[float(x) for x in r[1:]] for r in rows])
+    if biases:
+        return ids, vals[:, 0], vals[:, 1:]
+    return ids, vals
+
+
+def write_dataset(path, users, items, values):
+    with open(path, "w") as f:
+        for u, i, v in zip(users, items, values):
+            f.write("%d %d %r\n" % (u, i, float(v)))
+
+
+def write_dist(path, init):
+    with open(path, "w") as f:
+        f.write("".join("%.9f\n" % x for x in np.ravel(init)))
+
+
+# the log prints losses with ostream's default 6 significant digits, as the reference
+LOG_RTOL = 5e-6
+
+
+def losses(log):
+    return [float(x) for x in re.findall(r"epoch \d+: train loss = ([-\d.e+]+)", log)]
+
+
+def wals_vs_oracle(tmp_path, users, items, values, k, nepochs, precision, lam=0.05, alpha=40.0,
+                   init=None, extra=()):
+    data = str(tmp_path / "train.txt")
+    write_dataset(data, users, items, values)
+    o = po.OracleWALS(users, items, values, k, lam, alpha)
+    if init is None:
+        init = np.random.default_rng(k).uniform(-0.01, 0.01, (o.nitems, k))
+    dist = str(tmp_path / "dist.dat")
+    write_dist(dist, init)
+    o.load_distribution_file(dist)
+    uf, itf = str(tmp_path / "U.txt"), str(tmp_path / "I.txt")
+    log = run("wals", "--train_dataset=" + data, "--nfactors=%d" % k, "--nepochs=%d" % nepochs,
+              "--regularization_lambda=%r" % lam, "--confidence_weight=%r" % alpha,
+              "--distribution_file=" + dist, "--user_factors=" + uf, "--item_factors=" + itf,
+              "--precision=%d" % precision, *extra)
+    ol = o.optimize(nepochs)
+    ui, U = read_factors(uf)
+    ii, I = read_factors(itf)
+    assert np.array_equal(ui, o.ids(0)) and np.array_equal(ii, o.ids(1))
+    return log, ol, U, I, o
+
+
+@pytest.mark.parametrize("precision,tol,lam", [(64, 1e-8, 0.05), (32, 1e-3, 5.0)])
+def test_wals_cli_tiny(tmp_path, precision, tol, lam):
+    u, i, v = load_tiny()
+    log, ol, U, I, o = wals_vs_oracle(tmp_path, u, i, v, 8, 3, precision, lam=lam)
+    assert rel_err(U, o.factors(0)) < tol and rel_err(I, o.factors(1)) < tol
+    np.testing.assert_allclose(losses(log), ol, rtol=max(tol * 10, LOG_RTOL))
+
+
+@pytest.mark.parametrize("precision,tol", [(64, 1e-8), (32, 2e-3)])
+def test_wals_cli_ml100k_shape_matches_reference_losses(tmp_path, precision, tol):
+    d = load_ml100k()
+    k = 30
+    init = d["init"][: 1682 * k].reshape(1682, k)
+    log, ol, U, I, o = wals_vs_oracle(tmp_path, d["users"], d["items"], d["values"], k, 10,
+                                      precision, init=init)
+    ls = losses(log)
+    assert len(ls) == 10
+    # the reference's own printed losses, at 6 significant digits
+    assert abs(ls[0] - float(d["ref_loss_epoch1"])) < 1e-5 * (1 if precision == 64 else 10)
+    assert abs(ls[9] - float(d["ref_loss_epoch10"])) < 1e-6 * (1 if precision == 64 else 100)
+    assert rel_err(U, o.factors(0)) < tol and rel_err(I, o.factors(1)) < tol
+
+
+def test_wals_cli_indefinite_rows_fall_back_to_host(tmp_path):
+    # 1 + α·v < 0 with O(1) factors makes some user systems indefinite: the device flags
+    # them and the engine re-solves them on the host with a pivoted solve, where the
+    # reference's dsysv would run Bunch-Kaufman.  One user half + one item half.
+    u, i, v = synth(300, 80, 3000, seed=9)
+    v = v.copy()
+    v[::11] = -5.0
+    init = np.random.default_rng(1).uniform(0.2, 0.4, (80, 8))
+    log, ol, U, I, o = wals_vs_oracle(tmp_path, u, i, v, 8, 1, 64, lam=0.01, init=init)
+    assert "not positive definite; solving them on the host" in log
+    assert rel_err(U, o.factors(0)) < 1e-7 and rel_err(I, o.factors(1)) < 1e-7
+    np.testing.assert_allclose(losses(log), ol, rtol=LOG_RTOL)
+
+
+def test_wals_cli_test_metrics(tmp_path):
+    u, i, v = synth(400, 150, 6000, seed=3)
+    te = synth(400, 150, 1500, seed=30)
+    test = str(tmp_path / "test.txt")
+    write_dataset(test, *te)
+    log, ol, U, I, o = wals_vs_oracle(tmp_path, u, i, v, 16, 2, 64,
+                                      extra=("--test_dataset=" + test,
+                                             "--test_avg_metrics=auc,p@5,r@10,ap,mse"))
+    rec = dict(re.findall(r"recorded metric (\w+@?\d*) = ([-\d.e+]+)", log))
+    assert set(rec) == {"test_avg_auc", "test_avg_p@5", "test_avg_r@10", "test_avg_ap",
+                        "test_avg_mse"}
+    # AUC recomputed from the saved factors over every test user (numTestUsers = 0)
+    uid, iid = o.ids(0), o.ids(1)
+    L = {}
+    for a, b, w in zip(*te):
+        if a in set(uid) and b in set(iid):
+            L.setdefault(int(np.searchsorted(uid, a)), {})[int(np.searchsorted(iid, b))] = w
+    aucs = []
+    S = U @ I.T
+    for uu, labs in L.items():
+        lab = np.zeros(len(iid))
+        for it, w in labs.items():
+            lab[it] = w
+        pos, neg = S[uu][lab > 0], S[uu][lab <= 0]
+        if len(pos) == 0 or len(neg) == 0:
+            aucs.append(1.0)
+            continue
+        aucs.append(np.mean(pos[:, None] > neg[None, :]))
+    assert abs(float(rec["test_avg_auc"]) - np.mean(aucs)) < 1e-4
+
+
+def clustered(nusers, nitems, nnz, seed, groups=10):
+    """Users of group g mostly like items of group g: BPR has something to learn."""
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, nusers, nnz)
+    same = rng.random(nnz) < 0.8
+    i = np.where(same, (rng.integers(0, nitems // groups, nnz) * groups + u % groups) % nitems,
+                 rng.integers(0, nitems, nnz))
+    return u.astype(np.int64), i.astype(np.int64), np.ones(nnz)
+
+
+def bpr_pref_rate(tmp_path, dataset, checks, nfactors, trials=10):
+    data = str(tmp_path / "bpr.txt")
+    write_dataset(data, *zip(*[(a, b, 1.0) for a, b in dataset]))
+    ok = total = 0
+    for t in range(trials):
+        uf, itf = str(tmp_path / ("U%d" % t)), str(tmp_path / ("I%d" % t))
+        run("bpr", "--train_dataset=" + data, "--nepochs=40", "--nfactors=%d" % nfactors,
+            "--init_learning_rate=0.1", "--decay_rate=1.0", "--init_distribution_bound=0.1",
+            "--num_negative_samples=1", "--num_hogwild_threads=2", "--use_biases=false",
+            "--eval_num_neg=1", "--seed=%d" % (t + 1), "--user_factors=" + uf,
+            "--item_factors=" + itf)
+        ui, U = read_factors(uf)
+        ii, I = read_factors(itf)
+        uix = {int(x): n for n, x in enumerate(ui)}
+        iix = {int(x): n for n, x in enumerate(ii)}
+        for uu, p, n in checks:
+            total += 1
+            ok += float(U[uix[uu]] @ (I[iix[p]] - I[iix[n]])) > 0
+    return ok / total
+
+
+def test_bpr_cli_learns_preferences(tmp_path):
+    # BPREngineTest.cpp:80-157: > 90% of the preference checks hold
+    assert bpr_pref_rate(tmp_path, [(1, 1), (2, 2)], [(1, 1, 2), (2, 2, 1)], 1) > 0.9
+    ds = [(1, 1), (1, 3), (2, 2), (3, 1)]
+    ck = [(1, 1, 2), (1, 3, 2), (2, 2, 1), (2, 2, 3), (3, 1, 2), (3, 3, 2)]
+    assert bpr_pref_rate(tmp_path, ds, ck, 1) > 0.9
+    assert bpr_pref_rate(tmp_path, ds, ck, 3) > 0.9
+
+
+@pytest.mark.parametrize("precision", [32, 64])
+def test_bpr_cli_eval_losses_match_oracle(tmp_path, precision):
+    u, i, v = clustered(2000, 500, 30000, seed=8)
+    te = clustered(2000, 500, 5000, seed=80)
+    data, test = str(tmp_path / "tr.txt"), str(tmp_path / "te.txt")
+    write_dataset(data, u, i, v)
+    write_dataset(test, *te)
+    uf, itf = str(tmp_path / "U"), str(tmp_path / "I")
+    log = run("bpr", "--train_dataset=" + data, "--test_dataset=" + test, "--nepochs=5",
+              "--nfactors=16", "--use_biases", "--seed=3", "--precision=%d" % precision,
+              "--user_factors=" + uf, "--item_factors=" + itf)
+    pairs = re.findall(r"train loss = ([-\d.e+]+), test loss = ([-\d.e+]+)", log)
+    assert len(pairs) == 5
+    tr = [float(a) for a, _ in pairs]
+    te_l = [float(b) for _, b in pairs]
+    assert tr[-1] < tr[0] < np.log(2) and te_l[-1] < te_l[0] < np.log(2)  # learning
+    # the last logged losses equal the oracle's loss over the same evaluation sets, on the
+    # saved factors (9-decimal text)
+    _, _, ev, tev = po.bpr_sets(u, i, v, test=te, eval_num_neg=3, eval_seed=42)
+    ids_u, U = read_factors(uf)
+    ids_i, b, I = read_factors(itf, biases=True)
+    o_tr = po.bpr_loss_sum(U, I, b, ev, True) / len(ev)
+    o_te = po.bpr_loss_sum(U, I, b, tev, True) / len(tev)
+    assert abs(float(pairs[-1][0]) - o_tr) < 1e-5
+    assert abs(float(pairs[-1][1]) - o_te) < 1e-5
