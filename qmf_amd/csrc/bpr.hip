@@ -21,16 +21,30 @@ struct Row {
   T v[E];
 };
 
+// Factor rows and biases are shared by all waves of the epoch (Hogwild).  The per-CU vector
+// L1 is not coherent across CUs: a plain load can return a row another CU updated long
+// ago, and writing it back would erase that update.  Relaxed agent-scope atomics go to the
+// coherent L2 (no ordering is implied, exactly Hogwild's contract).
+template <typename T>
+__device__ __forceinline__ T ld_shared(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_shared(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T, int E>
 __device__ __forceinline__ void load_row(Row<T, E>& r, const T* base, int lane, int kp) {
 #pragma unroll
-  for (int e = 0; e < E; ++e) r.v[e] = (lane + 64 * e < kp) ? base[lane + 64 * e] : T(0);
+  for (int e = 0; e < E; ++e)
+    r.v[e] = (lane + 64 * e < kp) ? ld_shared(base + lane + 64 * e) : T(0);
 }
 template <typename T, int E>
 __device__ __forceinline__ void store_row(const Row<T, E>& r, T* base, int lane, int kp) {
 #pragma unroll
   for (int e = 0; e < E; ++e)
-    if (lane + 64 * e < kp) base[lane + 64 * e] = r.v[e];
+    if (lane + 64 * e < kp) st_shared(base + lane + 64 * e, r.v[e]);
 }
 
 // One SGD step on (u, p, n).  Returns false if the derivative was not finite.
@@ -48,8 +62,8 @@ __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t
   T x = wave_sum(part);
   T bp = T(0), bn = T(0);
   if (a.use_biases) {
-    bp = a.bias[p];
-    bn = a.bias[n];
+    bp = ld_shared(a.bias + p);
+    bn = ld_shared(a.bias + n);
     x += bp - bn;
   }
   const T ex = exp(x);
@@ -57,8 +71,8 @@ __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t
   if (!isfinite(eg)) return false;
   const T lr = a.lr;
   if (a.use_biases && lane == 0) {
-    a.bias[p] = bp + lr * (eg - a.bias_lambda * bp);
-    a.bias[n] = bn + lr * (-eg - a.bias_lambda * bn);
+    st_shared(a.bias + p, bp + lr * (eg - a.bias_lambda * bp));
+    st_shared(a.bias + n, bn + lr * (-eg - a.bias_lambda * bn));
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -164,10 +178,6 @@ __global__ void sum_partials_kernel(const double* partial, int n, double* out) {
   }
 }
 
-static int bpr_grid(int64_t npos) {
-  const int64_t g = 256 * 16;  // 16 waves per CU
-  return (int)(npos < g ? (npos > 0 ? npos : 1) : g);
-}
 
 #define QMFX_E_SWITCH(KP, CALL)          \
   switch ((KP + 63) / 64) {              \
@@ -180,7 +190,7 @@ static int bpr_grid(int64_t npos) {
 
 template <typename T, int E>
 static hipError_t bpr_epoch(const BprArgs<T>& a, hipStream_t s) {
-  hipLaunchKernelGGL((bpr_epoch_kernel<T, E>), dim3(bpr_grid(a.npos)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((bpr_epoch_kernel<T, E>), dim3(a.waves), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 template <typename T, int E>

@@ -150,7 +150,7 @@ hipError_t sort_unique_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int64_
   if (e == hipSuccess) e = hipcub::DeviceSelect::Unique(d_tmp, tmp_uniq, scratch, keys, d_num, (int)n, s);
   if (e == hipSuccess) e = hipMemcpyAsync(n_out, d_num, sizeof(int64_t), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  hipFreeAsync(d_tmp, s);
+  (void)hipFreeAsync(d_tmp, s);
   return e;
 }
 
@@ -164,7 +164,7 @@ hipError_t sort_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int end_bit, 
   if ((e = hipMallocAsync(&d_tmp, tmp + 16, s)) != hipSuccess) return e;
   e = hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp, keys, scratch, (int)n, 0, end_bit, s);
   if (e == hipSuccess) e = hipMemcpyAsync(keys, scratch, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
-  hipFreeAsync(d_tmp, s);
+  (void)hipFreeAsync(d_tmp, s);
   return e;
 }
 

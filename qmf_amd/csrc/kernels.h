@@ -67,6 +67,7 @@ struct BprArgs {
   int use_biases;
   int kp;                  // row stride (padded factors)
   int32_t* bad;            // set to 1 if a derivative was not finite
+  int waves;               // concurrent waves of the epoch kernel (Hogwild width)
 };
 
 hipError_t launch_bpr_epoch_f32(const BprArgs<float>& a, int kp, hipStream_t s);

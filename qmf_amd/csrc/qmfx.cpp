@@ -57,6 +57,7 @@ struct SideBuf {
   int64_t wb[5] = {0, 0, 0, 0, 0};
   int64_t n_ord = 0;
   double nnz_w = 0, nnz_d = 0;
+  double flops_w = 0;  // algorithmic flops of the whitened rows per half (see qmfx_wals_half)
   bool buckets_valid = false;
 };
 
@@ -204,13 +205,17 @@ int build_buckets(qmfx_ctx* c, int side) {
   const int mx = max_whitened_ntn(c);
   std::vector<int64_t> wlist[4];
   std::vector<std::pair<int64_t, int64_t>> direct;
-  double nnz_w = 0, nnz_d = 0;
+  double nnz_w = 0, nnz_d = 0, flops_w = 0;
+  const double k = c->k;
   for (int64_t r = sb.rbeg; r < sb.rend; ++r) {
     const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
     const int64_t ntn = (std::max<int64_t>(n, 1) + 15) / 16;
     if (ntn <= mx) {
       wlist[ntn - 1].push_back(r);
       nnz_w += (double)n;
+      // K (n(n+1)k), n×n Cholesky + solves (n³/3 + 2n²), Zᵀu and Zᵀc (4nk), unwhitening (2k²)
+      const double dn = (double)n;
+      flops_w += dn * (dn + 1) * k + dn * dn * dn / 3.0 + 2 * dn * dn + 4 * dn * k + 2 * k * k;
     } else {
       direct.emplace_back(n, r);
       nnz_d += (double)n;
@@ -229,6 +234,7 @@ int build_buckets(qmfx_ctx* c, int side) {
   sb.n_ord = (int64_t)order.size();
   sb.nnz_w = nnz_w;
   sb.nnz_d = nnz_d;
+  sb.flops_w = flops_w;
   if (sb.d_order) (void)hipFree(sb.d_order);
   sb.d_order = nullptr;
   HIPCHK(hipMalloc(&sb.d_order, (size_t)std::max<int64_t>(sb.n_ord, 1) * 8));
@@ -290,8 +296,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
 
 int qmfx_destroy(qmfx_ctx* c) {
   if (!c) return 0;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto& sb : c->s) {
     dfree_t(sb.rowptr);
@@ -305,7 +311,7 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree_t(c->rowloss);
   dfree_t(c->status);
   dfree_t(c->dsum);
-  if (c->hsum) hipHostFree(c->hsum);
+  if (c->hsum) (void)hipHostFree(c->hsum);
   dfree_t(c->bad);
   dfree_t(c->eval_partial);
   dfree_t(c->pos_user);
@@ -315,14 +321,14 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree(c->bias);
   dfree_t(c->trip[0]);
   dfree_t(c->trip[1]);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto& ev : c->evh)
-    if (ev) hipEventDestroy(ev);
+    if (ev) (void)hipEventDestroy(ev);
   dfree(c->Z);
   dfree(c->Linv);
   dfree_t(c->chol_status);
-  if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
 }
@@ -449,8 +455,8 @@ int qmfx_gen_synthetic(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz,
   HIPCHK(launch_synth_values_any(scratch, m, (uint64_t)nusers, (uint64_t)nitems, 0, seed * 31 + 7,
                                  c->s[1].val, c->prec, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  hipFree(keys);
-  hipFree(scratch);
+  (void)hipFree(keys);
+  (void)hipFree(scratch);
   for (int side = 0; side < 2; ++side) {
     SideBuf& sb = c->s[side];
     sb.h_rowptr.resize(sb.n + 1);
@@ -636,14 +642,9 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     c->cls_bytes[0] += by_d;
   }
   if (nW > 0 && use_w) {
-    // per whitened row with n signals: K (n(n+1)k), n×n Cholesky + solves (n³/3 + 2n²),
-    // Zᵀu and Zᵀc (4nk), unwhitening (2k²); bytes: gathers, x' write, x' read + x write
-    const int mx = max_whitened_ntn(c);
-    for (int64_t r = rb; r < re; ++r) {
-      const double n = (double)(L.h_rowptr[r + 1] - L.h_rowptr[r]);
-      if (((int64_t)std::max(n, 1.0) + 15) / 16 <= mx)
-        fl_w += n * (n + 1) * k + n * n * n / 3.0 + 2 * n * n + 4 * n * k + 2 * k * k;
-    }
+    // whitened-row flops precomputed per side in build_buckets; bytes: gathers, x' write,
+    // x' read + x write
+    fl_w = L.flops_w;
     by_w = nzw * (4 + s) + nzw * k * s + nw * k * s * 3 + nw * 16;
     c->cls_ms[1] += ms_w;
     c->cls_launches[1] += 1;
@@ -857,6 +858,12 @@ static BprArgs<T> bpr_args(qmfx_ctx* c, double lr, double bl, double ul, double 
   a.use_biases = ub;
   a.kp = c->kp;
   a.bad = c->bad;
+  // Hogwild width: concurrent waves collide when they touch the same user or item row, and
+  // a collision drops an update.  Keep the expected number of concurrent waves per row
+  // small: ≈ min(nusers, nitems)/16 waves, capped at 16 waves per CU (4096), at least 1
+  // (a 3-user problem runs serially, as the reference's 1-thread default does).
+  const int64_t rows = std::min(c->s[0].n, c->s[1].n);
+  a.waves = (int)std::max<int64_t>(1, std::min<int64_t>({4096, rows / 16, std::max<int64_t>(c->npos, 1)}));
   return a;
 }
 
@@ -934,7 +941,7 @@ int qmfx_bpr_apply(qmfx_ctx* c, const int64_t* trip, int64_t n, double lr, doubl
   int32_t bad = 0;
   HIPCHK(hipMemcpyAsync(&bad, c->bad, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  hipFree(d);
+  (void)hipFree(d);
   if (bad) return fail("gradients too big, try decreasing the learning rate (--init_learning_rate)", -4);
   return 0;
 }
@@ -1059,9 +1066,9 @@ int qmfx_selftest_mfma(int device, int precision, const double* A, const double*
     HIPCHK(launch_mfma_selftest_f64((double*)dA, (double*)dB, (double*)dC, nullptr));
     HIPCHK(hipMemcpy(C, dC, 2048, hipMemcpyDeviceToHost));
   }
-  hipFree(dA);
-  hipFree(dB);
-  hipFree(dC);
+  (void)hipFree(dA);
+  (void)hipFree(dB);
+  (void)hipFree(dC);
   return 0;
 }
 

@@ -395,16 +395,18 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   acc_t acc[NTT];
 #pragma unroll
   for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
+  if (!(a.ablate & 16)) {
 #pragma unroll
-  for (int q = 0; q < NTK; ++q) {
+    for (int q = 0; q < NTK; ++q) {
 #pragma unroll
-    for (int comp = 0; comp < 4; ++comp) {
+      for (int comp = 0; comp < 4; ++comp) {
 #pragma unroll
-      for (int I = 0; I < NTN; ++I) {
+        for (int I = 0; I < NTN; ++I) {
 #pragma unroll
-        for (int J = 0; J <= I; ++J) {
-          const int t = tile_index(I, J);
-          acc[t] = M::mma(zr[I][q][comp], zr[J][q][comp], acc[t]);
+          for (int J = 0; J <= I; ++J) {
+            const int t = tile_index(I, J);
+            acc[t] = M::mma(zr[I][q][comp], zr[J][q][comp], acc[t]);
+          }
         }
       }
     }
@@ -486,6 +488,10 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   for (int q = 0; q < NTK; ++q) {
 #pragma unroll
     for (int comp = 0; comp < 4; ++comp) {
+      if (a.ablate & 32) {
+        xp[q][comp] = zr[0][q][comp];
+        continue;
+      }
       T sx = T(0), sb = T(0);
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {

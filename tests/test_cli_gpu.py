@@ -183,28 +183,70 @@ def test_bpr_cli_learns_preferences(tmp_path):
     assert bpr_pref_rate(tmp_path, ds, ck, 3) > 0.9
 
 
+def sgd_simulation(uidx, iidx, nitems, k, epochs, lr, decay, lam, bound, use_biases, ev, tev,
+                   seed, num_neg=3):
+    """Serial reference SGD (oracle BPREngine::update over every positive × num_neg
+    rejection-sampled negatives, shuffled after each epoch, lr decay) → per-epoch mean eval
+    losses on the given triplet sets."""
+    rng = np.random.default_rng(seed)
+    nu = int(uidx.max()) + 1
+    U = rng.uniform(-bound, bound, (nu, k))
+    I = rng.uniform(-bound, bound, (nitems, k))
+    b = rng.uniform(-bound, bound, nitems) if use_biases else np.zeros(nitems)
+    pos = set((uidx * nitems + iidx).tolist())
+    order = np.arange(len(uidx))
+    out = []
+    for e in range(epochs):
+        uu = np.repeat(uidx[order], num_neg)
+        pp = np.repeat(iidx[order], num_neg)
+        nn = rng.integers(0, nitems, len(uu))
+        bad = np.array([x in pos for x in (uu * nitems + nn).tolist()])
+        while bad.any():
+            nn[bad] = rng.integers(0, nitems, int(bad.sum()))
+            bad[bad] = [x in pos for x in (uu[bad] * nitems + nn[bad]).tolist()]
+        po.bpr_update_seq(U, I, b, np.stack([uu, pp, nn], 1), lr, *lam, use_biases)
+        out.append((po.bpr_loss_sum(U, I, b, ev, use_biases) / len(ev),
+                    po.bpr_loss_sum(U, I, b, tev, use_biases) / len(tev)))
+        lr *= decay
+        order = rng.permutation(order)
+    return out
+
+
 @pytest.mark.parametrize("precision", [32, 64])
 def test_bpr_cli_eval_losses_match_oracle(tmp_path, precision):
+    """Exact: the logged evaluation losses equal the oracle's loss over the reference's
+    evaluation sets on the saved factors.  Statistical: the per-epoch loss trajectory of
+    the device Hogwild epochs tracks a serial reference-SGD simulation."""
     u, i, v = clustered(2000, 500, 30000, seed=8)
     te = clustered(2000, 500, 5000, seed=80)
     data, test = str(tmp_path / "tr.txt"), str(tmp_path / "te.txt")
     write_dataset(data, u, i, v)
     write_dataset(test, *te)
     uf, itf = str(tmp_path / "U"), str(tmp_path / "I")
-    log = run("bpr", "--train_dataset=" + data, "--test_dataset=" + test, "--nepochs=5",
-              "--nfactors=16", "--use_biases", "--seed=3", "--precision=%d" % precision,
+    hp = dict(epochs=8, lr=0.1, decay=0.9, lam=(1.0, 0.025, 0.0025), bound=0.1)
+    log = run("bpr", "--train_dataset=" + data, "--test_dataset=" + test,
+              "--nepochs=%d" % hp["epochs"], "--nfactors=16", "--use_biases", "--seed=3",
+              "--init_learning_rate=%r" % hp["lr"], "--decay_rate=%r" % hp["decay"],
+              "--init_distribution_bound=%r" % hp["bound"], "--precision=%d" % precision,
               "--user_factors=" + uf, "--item_factors=" + itf)
-    pairs = re.findall(r"train loss = ([-\d.e+]+), test loss = ([-\d.e+]+)", log)
-    assert len(pairs) == 5
-    tr = [float(a) for a, _ in pairs]
-    te_l = [float(b) for _, b in pairs]
-    assert tr[-1] < tr[0] < np.log(2) and te_l[-1] < te_l[0] < np.log(2)  # learning
-    # the last logged losses equal the oracle's loss over the same evaluation sets, on the
-    # saved factors (9-decimal text)
-    _, _, ev, tev = po.bpr_sets(u, i, v, test=te, eval_num_neg=3, eval_seed=42)
-    ids_u, U = read_factors(uf)
-    ids_i, b, I = read_factors(itf, biases=True)
-    o_tr = po.bpr_loss_sum(U, I, b, ev, True) / len(ev)
-    o_te = po.bpr_loss_sum(U, I, b, tev, True) / len(tev)
-    assert abs(float(pairs[-1][0]) - o_tr) < 1e-5
-    assert abs(float(pairs[-1][1]) - o_te) < 1e-5
+    pairs = [(float(a), float(b)) for a, b in
+             re.findall(r"train loss = ([-\d.e+]+), test loss = ([-\d.e+]+)", log)]
+    assert len(pairs) == hp["epochs"]
+    uids, iids, ev, tev = po.bpr_sets(u, i, v, test=te, eval_num_neg=3, eval_seed=42)
+    _, U = read_factors(uf)
+    _, b, I = read_factors(itf, biases=True)
+    assert abs(pairs[-1][0] - po.bpr_loss_sum(U, I, b, ev, True) / len(ev)) < 2e-6
+    assert abs(pairs[-1][1] - po.bpr_loss_sum(U, I, b, tev, True) / len(tev)) < 2e-6
+    # learning, and close to the serial reference SGD at every epoch
+    ui_map = {x: n for n, x in enumerate(uids.tolist())}
+    ii_map = {x: n for n, x in enumerate(iids.tolist())}
+    sim = sgd_simulation(np.array([ui_map[x] for x in u.tolist()]),
+                         np.array([ii_map[x] for x in i.tolist()]), len(iids), 16,
+                         hp["epochs"], hp["lr"], hp["decay"], hp["lam"], hp["bound"], True,
+                         ev, tev, seed=precision)
+    assert pairs[-1][0] < pairs[0][0] - 0.05
+    # Hogwild collisions cost most in epoch 1 (large gradients, 500 items); afterwards the
+    # device trajectory tracks the serial one closely
+    for e, ((dtr, dte), (str_, ste)) in enumerate(zip(pairs, sim)):
+        tol = 0.06 if e == 0 else 0.02
+        assert abs(dtr - str_) < tol and abs(dte - ste) < tol, (e, pairs, sim)
