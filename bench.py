@@ -87,6 +87,33 @@ def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
     return total, detail
 
 
+# kernels of each timed class (names as rocprofv3 reports them)
+CLASS_KERNELS = {
+    "wals_direct_kernel": ("wals_direct_kernel<",),
+    "wals_whitened (row solve + unwhiten)": ("wals_woodbury_kernel<", "whiten_kernel<{T}, {NT}, true>"),
+}
+
+
+def pmc_traffic(config, precision, cls, k):
+    """HBM bytes per class launch from the newest committed PMC summary for this workload
+    (profiles/rNN/pmc_<config>_<dtype>.json, written by tools/pmc_summary.py from
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes; fetch already doubled per the gfx950 note)."""
+    import glob
+    dt = "f32" if precision == 32 else "f64"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_%s_%s.json" % (config, dt))))
+    if not files:
+        return None, None
+    ks = json.load(open(files[-1]))["kernels"]
+    T = "float" if precision == 32 else "double"
+    pats = [p.format(T=T, NT=(k + 15) // 16) for p in CLASS_KERNELS[cls]]
+    tot, hit = 0.0, False
+    for name, e in ks.items():
+        if any(name.startswith(p) for p in pats) and "fetch_bytes" in e and "write_bytes" in e:
+            tot += e["fetch_bytes"] + e["write_bytes"]
+            hit = True
+    return (tot if hit else None), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,7 +194,11 @@ def main():
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": d["gbs"], "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(d["gbs"] / PEAK_HBM_GBS, 4)}
-    roof.update({"traffic": None, "launch_ms": d["launch_ms"], "classes": classes})
+    # per-dispatch means over the profiled run, like `achieved` (mean bytes per launch)
+    traffic, tsrc = pmc_traffic(args.config, args.precision, dom, k)
+    roof.update({"traffic": round(traffic, 0) if traffic else None,
+                 "traffic_algorithmic_ratio": round(traffic / d["bytes_per_launch"], 3) if traffic else None,
+                 "traffic_source": tsrc, "launch_ms": d["launch_ms"], "classes": classes})
     half = ctx.kernel_stats(2)
     epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
     hbm_frac_epoch = epoch_bytes / (ms_epoch / 1e3) / (PEAK_HBM_GBS * 1e9)
