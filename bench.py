@@ -26,7 +26,10 @@ CONFIGS = {
     "c3": (10_000_000, 1_000_000, 500_000_000, 128, 3),
     "c2": (1_000_000, 100_000, 50_000_000, 64, 2),
     "small": (200_000, 50_000, 10_000_000, 128, 5),
+    # BPR: C2's matrix, k=64, 3 negatives, lr 0.05, no biases
+    "c4": (1_000_000, 100_000, 50_000_000, 64, 2),
 }
+BPR_CONFIGS = {"c4"}
 LAM, ALPHA = 0.05, 40.0
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md
 PEAK_F64_TFLOPS = 78.6
@@ -114,6 +117,97 @@ def pmc_traffic(config, precision, cls, k):
     return (tot if hit else None), os.path.relpath(files[-1], ROOT)
 
 
+def eval_triplets(urp, ucol, ni, num_neg, seed):
+    """Every positive × num_neg negatives rejected against the user's positives (the
+    shape of BPREngine's evaluation set, BPREngine.cpp:85-87)."""
+    rng = np.random.default_rng(seed)
+    nu = len(urp) - 1
+    users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(urp))
+    u = np.repeat(users, num_neg)
+    p = np.repeat(ucol.astype(np.int64), num_neg)
+    keys = users * ni + ucol  # CSR rows are sorted by column: keys ascending
+    n = rng.integers(0, ni, len(u))
+    for _ in range(64):
+        q = u * ni + n
+        pos = np.searchsorted(keys, q)
+        bad = (pos < len(keys)) & (keys[np.minimum(pos, len(keys) - 1)] == q)
+        if not bad.any():
+            break
+        n[bad] = rng.integers(0, ni, int(bad.sum()))
+    return np.stack([u, p, n], 1)
+
+
+def bench_bpr(args, rank, world):
+    """C4: one step = one Hogwild epoch over every positive × 3 negatives (qmfx_bpr_epoch)
+    plus the evaluation-set loss (qmfx_bpr_eval), as BPREngine::optimize does per epoch."""
+    import qmf_amd
+    nu, ni, nnz_req, k, seed = CONFIGS[args.config]
+    num_neg, lr, lam = 3, 0.05, (1.0, 0.025, 0.0025)
+    ctx = qmf_amd.Context(k, args.precision, device=int(os.environ.get("LOCAL_RANK", "0")))
+    nnz = ctx.gen_synthetic(nu, ni, nnz_req, seed)
+    urp, ucol, _ = ctx.download_csr(0)
+    users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(urp))
+    # positives in a shuffled "file" order
+    perm = np.random.default_rng(seed).permutation(nnz)
+    ctx.bpr_set_positives(users[perm], ucol[perm].astype(np.int64))
+    ctx.fill_uniform(0, 0.01, seed + 100)
+    ctx.fill_uniform(1, 0.01, seed + 101)
+    ctx.bpr_set_biases(np.zeros(ni))
+    trip = eval_triplets(urp, ucol, ni, num_neg, seed)
+    del users, perm
+    ctx.sync()
+
+    def step(e):
+        ctx.bpr_epoch(seed * 1000 + e, num_neg, lr * 0.9 ** e, *lam, False, shuffle=e > 0)
+        return ctx.bpr_eval(0, trip, False) / len(trip)
+
+    for e in range(args.warmup):
+        step(e)
+    ctx.reset_stats()
+    ctx.sync()
+    t1 = time.perf_counter()
+    loss = 0.0
+    for e in range(args.steps):
+        loss = step(args.warmup + e)
+    ctx.sync()
+    el = time.perf_counter() - t1
+    st = ctx.solve_stats()
+    upd = nnz * num_neg * args.steps
+    sec = st["ms"] / 1e3 / max(st["launches"], 1)
+    by = st["bytes"] / max(st["launches"], 1)
+    out = {
+        "metric": "BPR Hogwild updates/sec at k=%d (epoch + evaluation pass)" % k,
+        "value": round(upd / el, 1), "unit": "updates/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "replicas", "vs_baseline": None,
+        "dtype": "f32" if args.precision == 32 else "f64",
+        "data": "synthetic (device-generated uniform unique pairs, seed %d)" % seed,
+        "config": {"workload": "%s: BPR %d users x %d items, %d positives x %d negatives, k=%d"
+                   % (args.config, nu, ni, nnz, num_neg, k)},
+        "roofline": {"kernel": "bpr_epoch_kernel", "bound": "hbm",
+                     "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                     "launch_ms": round(sec * 1e3, 3)},
+        "eval_loss": loss,
+    }
+    if not args.no_cpu_baseline and rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+        U, I = ctx.factors(0), ctx.factors(1)
+        b = np.zeros(ni)
+        sample = trip[np.random.default_rng(1).choice(len(trip), 3_000_000, replace=False)]
+        t0 = time.perf_counter()
+        po.bpr_update_seq(U, I, b, sample, lr, *lam, False)
+        t = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(sample) / t, 1), "unit": "updates/s", "cores": 1,
+                               "kind": "port",
+                               "sample": "oracle BPREngine::update, serial, on 3M of this "
+                                         "workload's triplets (%.1f s); the reference's "
+                                         "Hogwild default is 1 thread" % t}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,6 +220,11 @@ def main():
     args = ap.parse_args()
 
     import qmf_amd
+
+    if args.config in BPR_CONFIGS:
+        # BPR shards nothing (Hogwild across GPUs would need cross-device atomics): every
+        # rank runs an independent replica; rank 0 reports
+        return bench_bpr(args, int(os.environ.get("RANK", "0")), 1)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
