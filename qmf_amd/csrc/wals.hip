@@ -60,6 +60,58 @@ __device__ __forceinline__ double row16_sum(double v) {
 }
 
 // ---------------------------------------------------------------------------------------
+// fp32-accurate Gram on the bf16 matrix cores.  gfx950's f32-input MFMA runs at the f32
+// vector rate (64 flop/clk/SIMD); v_mfma_f32_16x16x32_bf16 does 16× that.  Each fp32 value
+// is split EXACTLY into three bf16 parts by truncation, x = hi + mid + lo (8 + 8 + 8
+// significand bits), and a product x·y is summed from the six parts of order ≤ 2:
+//   hi·hi + hi·mid + mid·hi + mid·mid + hi·lo + lo·hi
+// (each part product is exact in the fp32 accumulator; the dropped mid·lo + lo·mid + lo·lo
+// are ≤ 2⁻²³ relative — the size of fp32 rounding).  Six 16-cycle MFMAs per 16×16 tile and
+// 32 signals replace eight 32-cycle f32 MFMAs: 2.7× fewer matrix-core cycles.
+// Measured on gfx950 (tools/exp/bf16_layout.hip): Gram error 4.7e-7 of Σ|xᵢxⱼ| vs 2.5e-7
+// for an fp32 FMA chain.
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float trunc_bf16(float x) {
+  return __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+}
+// upper halves of (a, b) packed as two bf16: a in the low half, b in the high half
+__device__ __forceinline__ unsigned pack_hi16(float a, float b) {
+  return (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xffff0000u);
+}
+struct Split3 {
+  u32x4 h, m, l;
+};
+// 8 values (x[0..7]) → three bf16x8 operands with x = h + m + l exactly
+__device__ __forceinline__ void split3(const float (&x)[8], Split3& s) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float x0 = x[2 * p], x1 = x[2 * p + 1];
+    const float r0 = x0 - trunc_bf16(x0), r1 = x1 - trunc_bf16(x1);
+    const float l0 = r0 - trunc_bf16(r0), l1 = r1 - trunc_bf16(r1);
+    s.h[p] = pack_hi16(x0, x1);
+    s.m[p] = pack_hi16(r0, r1);
+    s.l[p] = pack_hi16(l0, l1);
+  }
+}
+__device__ __forceinline__ f32x4 mma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// acc += Xᵢ Xⱼᵀ to fp32 accuracy from the splits of the two row blocks
+__device__ __forceinline__ f32x4 mma_split6(const Split3& a, const Split3& b, f32x4 c) {
+  c = mma_bf16(a.h, b.h, c);
+  c = mma_bf16(a.h, b.m, c);
+  c = mma_bf16(a.m, b.h, c);
+  c = mma_bf16(a.m, b.m, c);
+  c = mma_bf16(a.h, b.l, c);
+  c = mma_bf16(a.l, b.h, c);
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------
 // Register-tile Cholesky + solve, shared by both row kernels (one wave64 per system).
 //   In:  acc = lower 16×16 tiles of an SPD matrix of size 16·NT (diagonal tiles full);
 //        S.bw = right-hand side (written and synchronised by the caller).
@@ -222,6 +274,124 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
   }
 }
 
+// Factor-index permutation of the fp32 direct path.  Lane column c of "virtual" block B
+// holds physical factor π(16B + c) = 16·W·(B / W) + W·c + (B mod W), so that one lane's
+// W consecutive physical factors (one 16·W-byte load) feed W different MFMA blocks.  The
+// Gram, the Cholesky and the right-hand side all live in the virtual order; the base
+// YᵀY + λI is read through π and x is scattered back through π.
+template <int NT>
+struct Perm {
+  static constexpr int W = (NT % 4 == 0) ? 4 : (NT % 2 == 0 ? 2 : 1);
+  // the split-bf16 Gram pays from NT = 6 up; at k ≤ 64 the f32 loop keeps 3 waves/SIMD
+  template <typename T>
+  static constexpr bool split = sizeof(T) == 4 && NT >= 6;
+  __device__ static __forceinline__ int phys(int v) {
+    const int B = v >> 4, c = v & 15;
+    return 16 * W * (B / W) + W * c + (B % W);
+  }
+};
+
+// Direct-row Gram, fp32 on the bf16 matrix cores: 32 signals per step, lane (c, g) owns
+// signals 8g..8g+7 of the step and virtual column c of every block.  Operands are √w·y
+// (w = αv ≥ 0), so A and B are the same split values: A += Σ w y yᵀ.  b = Σ c y and Σc
+// come from the raw rows.  Software pipeline: the column indices of step s+2 and the rows
+// of step s+1 are in flight while step s's MFMAs run.  A negative weight (1 + αv may still
+// be > 0) sets `negw`; the caller flags the row for the host solve.
+template <int NT>
+__device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64_t beg,
+                                                int64_t end, f32x4 (&acc)[NT * (NT + 1) / 2],
+                                                float (&bpart)[NT], double& csum, int& negw,
+                                                int lane) {
+  constexpr int KP = 16 * NT;
+  constexpr int W = Perm<NT>::W;
+  constexpr int NG = NT / W;
+  using vecW = float __attribute__((ext_vector_type(W)));
+  const int c = lane & 15;
+  const int g = lane >> 4;
+  // per step: column index and value of the lane's 8 signals, rows as W-vectors
+  int col0[8], col1[8];
+  float val0[8], val1[8];
+  vecW y0[8][NG], y1[8][NG];
+  auto load_meta = [&](int64_t base, int (&col)[8], float (&val)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t e = base + 8 * g + j;
+      const bool ok = e < end;
+      col[j] = ok ? a.col[e] : -1;
+      val[j] = ok ? a.val[e] : 0.f;
+    }
+  };
+  auto load_rows = [&](const int (&col)[8], vecW (&y)[8][NG]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const vecW* yr = reinterpret_cast<const vecW*>(a.Y + (int64_t)(col[j] < 0 ? 0 : col[j]) * KP) + c;
+#pragma unroll
+      for (int G = 0; G < NG; ++G) {
+        const vecW v = yr[16 * G];
+        y[j][G] = col[j] < 0 ? vecW{} : v;
+      }
+    }
+  };
+  load_meta(beg, col0, val0);
+  load_rows(col0, y0);
+  if (beg + 32 < end) load_meta(beg + 32, col1, val1);
+  float cs = 0.f;
+  for (int64_t base = beg; base < end; base += 32) {
+    const bool more = base + 32 < end;
+    int col2[8];
+    float val2[8];
+    if (more) {
+      load_rows(col1, y1);
+      if (base + 64 < end) load_meta(base + 64, col2, val2);
+    }
+    float sw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float w = a.alpha * val0[j];
+      const float cw = col0[j] >= 0 ? 1.f + w : 0.f;
+      negw |= w < 0.f;
+      sw[j] = fast_sqrt(fabsf(w));
+      cs += cw;
+#pragma unroll
+      for (int G = 0; G < NG; ++G)
+#pragma unroll
+        for (int m = 0; m < W; ++m) bpart[W * G + m] += cw * y0[j][G][m];
+    }
+    Split3 sp[NT];
+#pragma unroll
+    for (int G = 0; G < NG; ++G) {
+#pragma unroll
+      for (int m = 0; m < W; ++m) {
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = sw[j] * y0[j][G][m];
+        split3(x, sp[W * G + m]);
+      }
+    }
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        acc[t] = mma_split6(sp[I], sp[J], acc[t]);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        col0[j] = col1[j];
+        val0[j] = val1[j];
+        col1[j] = col2[j];
+        val1[j] = val2[j];
+#pragma unroll
+        for (int G = 0; G < NG; ++G) y0[j][G] = y1[j][G];
+      }
+    }
+  }
+  // each signal's c is held by the 16 lanes of its group: count it once
+  csum += (double)(c == 0 ? cs : 0.f);
+}
+
 // ---------------------------------------------------------------------------------------
 // Direct row kernel: one wave64 per row.  Gram A = G + λI + Σ w y yᵀ by 16x16x4 MFMAs into
 // the lower tiles held in registers; b = Σ c y and Σc on the side.  A row's (col, v) pairs
@@ -229,11 +399,13 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
 // gathers of step s+1 are in flight while the MFMAs of step s run.
 // ---------------------------------------------------------------------------------------
 #ifndef QMFX_WAVES_NT8
-#define QMFX_WAVES_NT8 2
+#define QMFX_WAVES_NT8 1
 #endif
 template <typename T, int NT>
-__global__ __launch_bounds__(64, (NT >= 8 && sizeof(T) == 4) ? QMFX_WAVES_NT8 : 2)
+__global__ __launch_bounds__(64, Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : 2)
 void wals_direct_kernel(SolveArgs<T> a) {
+  // fp32 at NT = 8: the split-bf16 Gram keeps 144 accumulator + 96 operand + 128 row
+  // registers live: one wave per SIMD with the whole register file (QMFX_WAVES_NT8 = 1)
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   constexpr int KP = 16 * NT;
@@ -258,8 +430,11 @@ void wals_direct_kernel(SolveArgs<T> a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = M::crow(lane, r);
-        T g = a.G[(int64_t)(16 * I + i) * KP + 16 * J + cl];
-        if (I == J && i == cl) g += (16 * I + i < a.k) ? a.lambda : T(1);
+        // fp32: the virtual (permuted) index space of gram_split_bf16
+        const int pi = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * I + i) : 16 * I + i;
+        const int pj = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * J + cl) : 16 * J + cl;
+        T g = a.G[(int64_t)pi * KP + pj];
+        if (I == J && i == cl) g += (pi < a.k) ? a.lambda : T(1);
         acc[t][r] = g;
       }
     }
@@ -268,6 +443,10 @@ void wals_direct_kernel(SolveArgs<T> a) {
 #pragma unroll
   for (int c = 0; c < NT; ++c) bpart[c] = T(0);
   double csum = 0.0;
+  int negw = 0;
+  if constexpr (Perm<NT>::template split<T>) {
+    if (!(a.ablate & 1)) gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
+  } else
   for (int64_t base = beg; base < end && !(a.ablate & 1); base += 64) {
     const int nst = (int)(end - base < 64 ? end - base : 64);
     const int cr = lane < nst ? a.col[base + lane] : 0;
@@ -319,14 +498,14 @@ void wals_direct_kernel(SolveArgs<T> a) {
     }
   }
   csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
-  int bad = 0;
+  int bad = __any(negw) ? 1 : 0;  // negative weight: solved on the host
   __syncthreads();
   chol_solve<T, NT>(acc, S, lane, bad, a.ablate);
 
   double xb = 0.0, xx = 0.0;
   for (int i = lane; i < KP; i += 64) {
     const T xi = S.xs[i];
-    a.X[row * KP + i] = xi;
+    a.X[row * KP + (Perm<NT>::template split<T> ? Perm<NT>::phys(i) : i)] = xi;
     xb += (double)xi * (double)borig[i];
     xx += (double)xi * (double)xi;
   }
