@@ -27,6 +27,13 @@ struct SolveArgs {
 
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s);
+// multi-wave row solve and strip YᵀY for large factor counts (wals_big.hip; nt 5..16)
+hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s);
+hipError_t launch_wals_big(const SolveArgs<double>& a, int nt, hipStream_t s);
+hipError_t launch_gram_big(const float* Y, int64_t n, int nt, float* G, double* partial,
+                           int max_blocks, hipStream_t s);
+hipError_t launch_gram_big(const double* Y, int64_t n, int nt, double* G, double* partial,
+                           int max_blocks, hipStream_t s);
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,

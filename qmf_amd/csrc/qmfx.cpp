@@ -188,8 +188,12 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 
 // Largest whitened-row bucket (NTN) usable for this factor tiling: n padded to 16 must be
 // at most 64 and at most KP/2 (beyond that the k×k solve is the cheaper one).
+// Factor counts beyond one wave's registers (fp32 k > 128, fp64 k > 64) use the multi-wave
+// row kernel and the strip YᵀY (wals_big.hip).
+bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
+
 int max_whitened_ntn(const qmfx_ctx* c) {
-  if (!c->whitened_enabled) return 0;
+  if (!c->whitened_enabled || use_big(c)) return 0;
   int m = c->nt / 2;
   if (m > 4) m = 4;
   if (c->prec == 64 && m > 2) m = 2;
@@ -260,9 +264,9 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (precision != 32 && precision != 64) return fail("precision must be 32 or 64");
   if (nfactors <= 0) return fail("nfactors must be positive");
   const int nt = (nfactors + 15) / 16;
-  if (precision == 32 && nt > 8) return fail("nfactors > 128 not supported in fp32 yet");
-  if (precision == 64 && nt > 4) return fail("nfactors > 64 not supported in fp64 yet");
+  if (nt > 16) return fail("nfactors > 256 not supported yet");
   auto* c = new qmfx_ctx();
+  if (nt > 8) c->gpart_blocks = 256;  // YᵀY partials: NTT·256 doubles per block
   c->device = device;
   c->prec = precision;
   c->k = nfactors;
@@ -538,12 +542,17 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   const bool fp32 = c->prec == 32;
   HIPCHK(hipEventRecord(c->evh[0], c->stream));
   // G = YᵀY of the fixed side (full replica on every rank)
+  const bool big = use_big(c);
   if (fp32)
-    HIPCHK(launch_gram((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart, c->gpart_blocks,
-                       c->stream));
+    HIPCHK(big ? launch_gram_big((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart,
+                                 c->gpart_blocks, c->stream)
+               : launch_gram((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart,
+                             c->gpart_blocks, c->stream));
   else
-    HIPCHK(launch_gram((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart, c->gpart_blocks,
-                       c->stream));
+    HIPCHK(big ? launch_gram_big((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
+                                 c->gpart_blocks, c->stream)
+               : launch_gram((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
+                             c->gpart_blocks, c->stream));
   if (use_w) {
     if (c->z_cap < R.n) {
       dfree(c->Z);
@@ -572,12 +581,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
                        (float*)L.F, c->rowloss, c->status, L.d_order, d_begin, nD,
                        (float)alpha, (float)lambda, c->k, c->ablate};
-    HIPCHK(launch_wals_direct(a, c->nt, c->stream));
+    HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   } else {
     SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
                         (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
                         d_begin, nD, alpha, lambda, c->k, c->ablate};
-    HIPCHK(launch_wals_direct(a, c->nt, c->stream));
+    HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²

@@ -1,0 +1,468 @@
+// WALS row solve for large factor counts (fp32 k > 128, fp64 k > 64; up to k = 256).
+//
+// Reference path: WALSEngine::updateFactorsForOne (qmf/wals/WALSEngine.cpp:266-310) and
+// linearSymmetricSolve → dsysv_ (qmf/Matrix.cpp:81-96), as in wals.hip.  At large k one
+// wave cannot hold the k×k system in registers, so one WORKGROUP of NW waves solves a row:
+//
+//   * the NT(NT+1)/2 lower 16×16 tiles of A are distributed round-robin over the waves and
+//     stay in their registers for the whole solve;
+//   * Gram: the row's fixed-side rows are staged into LDS SIG signals at a time (double
+//     buffer, register-staged loads of the next stage in flight during the MFMAs); every
+//     wave reads its tiles' operands from LDS, so the tile→wave map is a runtime table;
+//   * Cholesky, right-looking over 16-column panels: owners write panel column p to LDS,
+//     wave 0 factors it (streamed 64 rows at a time: register cost independent of k) and
+//     forward-solves b, then every wave applies the rank-16 trailing update to its own
+//     tiles with MFMA (operands from the LDS panel) — three barriers per panel;
+//   * backward solve by 16-blocks: owners of L(J, I) tiles add their part of Lᵀx in LDS,
+//     wave 0 finishes the block with the diagonal triangle.
+// Same results contract as the single-wave kernels: status[row] = 1 on a non-positive pivot.
+#include "common.h"
+#include "kernels.h"
+#include "rowsolve.h"
+
+namespace qmfx {
+
+template <typename T, int NT>
+struct BigCfg {
+  static constexpr int KP = 16 * NT;
+  static constexpr int NTT = NT * (NT + 1) / 2;
+  // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave
+  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : 8) : (NT <= 8 ? 4 : 8);
+  static constexpr int TPW = (NTT + NW - 1) / NW;
+  static constexpr int NTHR = 64 * NW;
+  static constexpr int SIG = sizeof(T) == 4 ? 32 : 16;  // signals per LDS stage
+  static constexpr int VEC = 16 / sizeof(T);             // elements per 16-B load
+  static constexpr int CPR = KP / VEC;                   // 16-B chunks per row
+  static constexpr int TRIPS = (SIG * CPR + NTHR - 1) / NTHR;
+  static constexpr int PLD = 17;                         // padded LDS row of a panel
+};
+
+template <typename T, int NT>
+struct BigShared {
+  using C = BigCfg<T, NT>;
+  T stage[2][C::SIG * C::KP];
+  T w[2][C::SIG];   // α·v of the staged signals (0 past the row end)
+  T c[2][C::SIG];   // 1 + α·v (0 past the row end)
+  T panel[C::KP * C::PLD];
+  T Ldiag[NT * 16 * C::PLD];
+  T bw[C::KP];
+  T borig[C::KP];
+  T xs[C::KP];
+  T invd[C::KP];
+  T part[C::NW * 16];
+  double red[C::NW];
+};
+
+// Panel p of the right-looking Cholesky, by ONE wave: rows 16p..KP-1 of column block p are
+// in S.panel (row q at q·PLD), the right-hand side in S.bw.  Factors the 16×16 diagonal
+// block (L, 1/diag in S.invd), solves the rows below against it, applies the forward
+// substitution to b, writes L back to S.panel and the diagonal block to S.Ldiag.
+// Rows are processed 64 per slot; slot 0 holds the diagonal block.
+template <typename T, int NT>
+__device__ void big_panel(BigShared<T, NT>& S, int p, int lane, int& bad) {
+  constexpr int KP = 16 * NT;
+  constexpr int PLD = BigCfg<T, NT>::PLD;
+  const int R = KP - 16 * p;
+  const int cl = lane & 15;
+  // slot 0: rows 0..63 (diagonal block + up to 48 rows below)
+  {
+    const int q = lane;
+    const bool live = q < R;
+    T pa[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
+    T pb = live ? S.bw[16 * p + q] : T(0);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const T d = readlane(pa[c], c);
+      bad |= !(d > T(0));
+      const T ljj = fast_sqrt(d);
+      const T inv = fast_rcp(ljj);
+      if (lane == 0) S.invd[16 * p + c] = inv;
+      const T lq = q > c ? pa[c] * inv : T(0);
+      pa[c] = q > c ? lq : (q == c ? ljj : pa[c]);
+      const T yc = readlane(pb, c) * inv;
+      if (lane == 0) S.bw[16 * p + c] = yc;
+      pb -= lq * yc;
+#pragma unroll
+      for (int m = c + 1; m < 16; ++m) pa[m] -= lq * readlane(lq, m);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (live) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
+      if (q >= 16) S.bw[16 * p + q] = pb;
+    }
+    for (int idx = lane; idx < 256; idx += 64) {
+      const int r = idx >> 4, c = idx & 15;
+      S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
+    }
+  }
+  // further slots: L(q, :) = A(q, :) · L_diag⁻ᵀ column by column, and b(q) -= L(q, c)·y_c
+  for (int base = 64; base < R; base += 64) {
+    const int q = base + lane;
+    const bool live = q < R;
+    T pa[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
+    T pb = live ? S.bw[16 * p + q] : T(0);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const T lq = pa[c] * S.invd[16 * p + c];
+      pa[c] = lq;
+      pb -= lq * S.bw[16 * p + c];
+#pragma unroll
+      for (int m = c + 1; m < 16; ++m) pa[m] -= lq * S.Ldiag[(p * 16 + m) * PLD + c];
+    }
+    if (live) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
+      S.bw[16 * p + q] = pb;
+    }
+  }
+  (void)cl;
+}
+
+template <typename T, int NT>
+__global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
+  using C = BigCfg<T, NT>;
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  using vec_t = T __attribute__((ext_vector_type(C::VEC)));
+  constexpr int KP = C::KP, NW = C::NW, TPW = C::TPW, NTT = C::NTT, SIG = C::SIG;
+  constexpr int CPR = C::CPR, TRIPS = C::TRIPS, PLD = C::PLD;
+  __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
+
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const int64_t slot = a.row_begin + blockIdx.x;
+  const int64_t row = a.order ? a.order[slot] : slot;
+  const int64_t beg = a.rowptr[row];
+  const int64_t end = a.rowptr[row + 1];
+
+  // this wave's tiles: t = wv + NW·s, (I, J) with t = I(I+1)/2 + J
+  int TI[TPW], TJ[TPW];
+#pragma unroll
+  for (int s = 0; s < TPW; ++s) {
+    const int t = wv + NW * s;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    TI[s] = t < NTT ? I : -1;
+    TJ[s] = t < NTT ? t - I * (I + 1) / 2 : -1;
+  }
+  acc_t acc[TPW];
+#pragma unroll
+  for (int s = 0; s < TPW; ++s) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * TI[s] + M::crow(lane, r), j = 16 * TJ[s] + cl;
+      T g = TI[s] >= 0 ? a.G[(int64_t)i * KP + j] : T(0);
+      if (TI[s] >= 0 && i == j) g += (i < a.k) ? a.lambda : T(1);
+      acc[s][r] = g;
+    }
+  }
+
+  // ---- Gram: A += Σ w y yᵀ, b = Σ c y, Σc -------------------------------------------------
+  int cols[TRIPS];
+  vec_t stg[TRIPS];
+  T wmeta = T(0), cmeta = T(0);
+  auto load_cols = [&](int64_t sb) {
+#pragma unroll
+    for (int t = 0; t < TRIPS; ++t) {
+      const int ch = tid + C::NTHR * t;
+      const int64_t e = sb + ch / CPR;
+      cols[t] = (ch < SIG * CPR && e < end) ? a.col[e] : -1;
+    }
+  };
+  auto load_rows = [&]() {
+#pragma unroll
+    for (int t = 0; t < TRIPS; ++t) {
+      const int ch = tid + C::NTHR * t;
+      const vec_t* src = reinterpret_cast<const vec_t*>(a.Y + (int64_t)(cols[t] < 0 ? 0 : cols[t]) * KP) + ch % CPR;
+      const vec_t v = *src;
+      stg[t] = cols[t] >= 0 ? v : vec_t{};
+    }
+  };
+  auto load_meta = [&](int64_t sb) {
+    const int64_t e = sb + tid;
+    const bool ok = tid < SIG && e < end;
+    const T v = ok ? a.val[e] : T(0);
+    wmeta = ok ? a.alpha * v : T(0);
+    cmeta = ok ? T(1) + a.alpha * v : T(0);
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < TRIPS; ++t) {
+      const int ch = tid + C::NTHR * t;
+      if (ch < SIG * CPR) reinterpret_cast<vec_t*>(S.stage[buf])[ch] = stg[t];
+    }
+    if (tid < SIG) {
+      S.w[buf][tid] = wmeta;
+      S.c[buf][tid] = cmeta;
+    }
+  };
+
+  T bp = T(0);        // b[tid] for tid < KP
+  double cs = 0.0;    // Σc (thread 0)
+  const int nstages = (int)((end - beg + SIG - 1) / SIG);
+  if (nstages > 0 && !(a.ablate & 1)) {
+    load_cols(beg);
+    load_rows();
+    load_meta(beg);
+    store_stage(0);
+    if (nstages > 1) load_cols(beg + SIG);
+    __syncthreads();
+    for (int st = 0; st < nstages; ++st) {
+      const int buf = st & 1;
+      const bool more = st + 1 < nstages;
+      if (more) {
+        load_rows();  // rows of stage st+1 (columns already in registers)
+        load_meta(beg + (int64_t)(st + 1) * SIG);
+      }
+      // MFMAs of stage st: 4 signals per step, operands straight from LDS
+      const T* sg = S.stage[buf];
+#pragma unroll 2
+      for (int k4 = 0; k4 < SIG; k4 += 4) {
+        const T* yk = sg + (k4 + kk) * KP + cl;
+        const T wk = S.w[buf][k4 + kk];
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+          if (TI[s] >= 0) {
+            const T ya = yk[16 * TI[s]];
+            const T yb = wk * yk[16 * TJ[s]];
+            acc[s] = M::mma(ya, yb, acc[s]);
+          }
+        }
+      }
+      if (tid < KP) {
+#pragma unroll 4
+        for (int k = 0; k < SIG; ++k) bp += S.c[buf][k] * sg[k * KP + tid];
+      }
+      if (tid == 0) {
+        for (int k = 0; k < SIG; ++k) cs += (double)S.c[buf][k];
+      }
+      if (more) {
+        store_stage(buf ^ 1);
+        if (st + 2 < nstages) load_cols(beg + (int64_t)(st + 2) * SIG);
+      }
+      __syncthreads();
+    }
+  }
+  if (tid < KP) {
+    S.bw[tid] = bp;
+    S.borig[tid] = bp;
+  }
+  __syncthreads();
+
+  // ---- Cholesky A = L Lᵀ with the forward solve of b folded in --------------------------
+  int bad = 0;
+  for (int p = 0; p < NT; ++p) {
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      if (TJ[s] == p) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          S.panel[(16 * (TI[s] - p) + M::crow(lane, r)) * PLD + cl] = acc[s][r];
+      }
+    }
+    __syncthreads();
+    if (wv == 0 && !(a.ablate & 2)) big_panel<T, NT>(S, p, lane, bad);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      if (TJ[s] == p && TI[s] > p) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[s][r] = S.panel[(16 * (TI[s] - p) + M::crow(lane, r)) * PLD + cl];
+      } else if (TJ[s] > p && !(a.ablate & 4)) {
+        const T* li = S.panel + (16 * (TI[s] - p) + cl) * PLD + kk;
+        const T* lj = S.panel + (16 * (TJ[s] - p) + cl) * PLD + kk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[s] = M::mma(-li[4 * q], lj[4 * q], acc[s]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- backward solve Lᵀ x = y ----------------------------------------------------------
+  for (int I = NT - 1; I >= 0 && !(a.ablate & 8); --I) {
+    T part = T(0);
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      if (TJ[s] == I && TI[s] > I) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part += acc[s][r] * S.xs[16 * TI[s] + M::crow(lane, r)];
+      }
+    }
+    part += shfl_xor(part, 16);
+    part += shfl_xor(part, 32);
+    if (kk == 0) S.part[wv * 16 + cl] = part;
+    __syncthreads();
+    if (wv == 0) {
+      T vm = S.bw[16 * I + cl];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) vm -= S.part[w * 16 + cl];
+      T lc[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) lc[c] = S.Ldiag[(I * 16 + c) * PLD + cl];
+#pragma unroll
+      for (int c = 15; c >= 0; --c) {
+        const T xc = readlane(vm, c) * S.invd[16 * I + c];
+        if (lane == 0) S.xs[16 * I + c] = xc;
+        if (cl < c) vm -= lc[c] * xc;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- output: x, row loss = Σc − xᵀb − λ‖x‖² ----------------------------------------------
+  double xb = 0.0, xx = 0.0;
+  if (tid < KP) {
+    const T xi = S.xs[tid];
+    a.X[row * KP + tid] = xi;
+    xb = (double)xi * (double)S.borig[tid];
+    xx = (double)xi * (double)xi;
+  }
+  const double contrib = wave_sum(xb + (double)a.lambda * xx);
+  if (lane == 0) S.red[wv] = contrib;
+  __syncthreads();
+  if (tid == 0) {  // wave 0 owns `bad` (set by its panel factorizations) and Σc
+    double t = 0.0;
+    for (int w = 0; w < NW; ++w) t += S.red[w];
+    a.rowloss[row] = bad ? 0.0 : cs - t;
+    if (bad && a.status) a.status[row] = 1;
+  }
+}
+
+// ---- YᵀY for large NT: one block row I of the lower triangle per blockIdx.y ---------------
+template <typename T, int NT>
+__global__ __launch_bounds__(64) void gram_strip_kernel(const T* Y, int64_t n,
+                                                        int64_t rows_per_block,
+                                                        double* partial) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  constexpr int KP = 16 * NT;
+  constexpr int NTT = NT * (NT + 1) / 2;
+  const int I = blockIdx.y;
+  const int lane = threadIdx.x;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  acc_t acc[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) acc[J] = acc_t{0, 0, 0, 0};
+  for (int64_t e0 = r0; e0 < r1; e0 += 4) {
+    const int64_t e = e0 + kk;
+    const bool valid = e < r1;
+    const T* yrow = Y + (valid ? e : r0) * KP + cl;
+    const T ya = valid ? yrow[16 * I] : T(0);
+#pragma unroll
+    for (int J = 0; J < NT; ++J) {
+      if (J <= I) {
+        const T yb = valid ? yrow[16 * J] : T(0);
+        acc[J] = M::mma(ya, yb, acc[J]);
+      }
+    }
+  }
+  double* out = partial + (int64_t)blockIdx.x * NTT * 256;
+#pragma unroll
+  for (int J = 0; J < NT; ++J) {
+    if (J <= I) {
+      const int t = tile_index(I, J);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[t * 256 + M::crow(lane, r) * 16 + cl] = (double)acc[J][r];
+    }
+  }
+}
+
+// fixed-order fp64 sum of the per-block partials + mirror (runtime NT)
+template <typename T>
+__global__ void gram_reduce_rt_kernel(const double* partial, int nblocks, int nt, T* G) {
+  const int KP = 16 * nt;
+  const int NTT = nt * (nt + 1) / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= KP * KP) return;
+  const int i = idx / KP, j = idx % KP;
+  const int ii = i >= j ? i : j, jj = i >= j ? j : i;
+  const int t = tile_index(ii >> 4, jj >> 4);
+  const int off = t * 256 + (ii & 15) * 16 + (jj & 15);
+  double sum = 0.0;
+  for (int b = 0; b < nblocks; ++b) sum += partial[(int64_t)b * NTT * 256 + off];
+  G[idx] = (T)sum;
+}
+
+template <typename T, int NT>
+static hipError_t launch_big_nt(const SolveArgs<T>& a, hipStream_t s) {
+  if (a.nrows <= 0) return hipSuccess;
+  hipLaunchKernelGGL((wals_big_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(BigCfg<T, NT>::NTHR),
+                     0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int NT>
+static hipError_t launch_gram_strip_nt(const T* Y, int64_t n, double* partial, int nblocks,
+                                       int64_t rows_per_block, hipStream_t s) {
+  if (nblocks > 0)
+    hipLaunchKernelGGL((gram_strip_kernel<T, NT>), dim3(nblocks, NT), dim3(64), 0, s, Y, n,
+                       rows_per_block, partial);
+  return hipGetLastError();
+}
+
+#define QMFX_BIG_SWITCH(NTV, CALL)        \
+  switch (NTV) {                          \
+    case 5: return CALL(5);               \
+    case 6: return CALL(6);               \
+    case 7: return CALL(7);               \
+    case 8: return CALL(8);               \
+    case 9: return CALL(9);               \
+    case 10: return CALL(10);             \
+    case 11: return CALL(11);             \
+    case 12: return CALL(12);             \
+    case 13: return CALL(13);             \
+    case 14: return CALL(14);             \
+    case 15: return CALL(15);             \
+    case 16: return CALL(16);             \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s) {
+#define CALL(N) launch_big_nt<float, N>(a, s)
+  QMFX_BIG_SWITCH(nt, CALL)
+#undef CALL
+}
+hipError_t launch_wals_big(const SolveArgs<double>& a, int nt, hipStream_t s) {
+#define CALL(N) launch_big_nt<double, N>(a, s)
+  QMFX_BIG_SWITCH(nt, CALL)
+#undef CALL
+}
+template <typename T>
+static hipError_t gram_big(const T* Y, int64_t n, int nt, T* G, double* partial, int max_blocks,
+                           hipStream_t s) {
+  int64_t rpb = (n + max_blocks - 1) / max_blocks;
+  rpb = ((rpb + 3) / 4) * 4;
+  if (rpb < 64) rpb = 64;
+  const int nblocks = (int)((n + rpb - 1) / rpb);
+  hipError_t e = hipSuccess;
+#define CALL(N) launch_gram_strip_nt<T, N>(Y, n, partial, nblocks, rpb, s)
+  e = [&]() -> hipError_t { QMFX_BIG_SWITCH(nt, CALL) }();
+#undef CALL
+  if (e != hipSuccess) return e;
+  const int KP = 16 * nt;
+  hipLaunchKernelGGL((gram_reduce_rt_kernel<T>), dim3((KP * KP + 255) / 256), dim3(256), 0, s,
+                     partial, nblocks, nt, G);
+  return hipGetLastError();
+}
+hipError_t launch_gram_big(const float* Y, int64_t n, int nt, float* G, double* partial,
+                           int max_blocks, hipStream_t s) {
+  return gram_big(Y, n, nt, G, partial, max_blocks, s);
+}
+hipError_t launch_gram_big(const double* Y, int64_t n, int nt, double* G, double* partial,
+                           int max_blocks, hipStream_t s) {
+  return gram_big(Y, n, nt, G, partial, max_blocks, s);
+}
+
+}  // namespace qmfx

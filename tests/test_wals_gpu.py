@@ -167,3 +167,25 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, monkeypatch):
         assert abs(lw - lo) < tol * abs(lo) * 10 and abs(ld - lo) < tol * abs(lo) * 10
         c.set_factors(side, o.factors(side))
         cd.set_factors(side, o.factors(side))
+
+
+@pytest.mark.parametrize("k,precision", [(144, 32), (192, 32), (256, 32), (80, 64), (128, 64),
+                                         (200, 64)])
+def test_large_k_multiwave_rows(k, precision):
+    """k beyond one wave's registers (fp32 > 128, fp64 > 64): the multi-wave row kernel
+    (LDS-staged Gram, distributed Cholesky) and the strip YᵀY, against the oracle; rows
+    from 1 to ~150 signals cover partial LDS stages and every panel-slot count."""
+    u, i, v = synth(1500, 300, 40000, seed=k)
+    # fp32 error ≈ cond·6e-8: at k = 256 these item systems have cond ≈ 2e4 at λ = 5, where
+    # a float32 LAPACK solve of the same systems is itself off by 2.5e-4 (this kernel: 1.4e-4).
+    # fp32 is therefore checked at a well-conditioned λ; fp64 (the logic check, 1e-9) at the
+    # reference λ.
+    lam = 0.05 if precision == 64 else 50.0
+    o, c = make_pair(u, i, v, k, precision, seed=3, lam=lam)
+    tol = 1e-9 if precision == 64 else 1e-4
+    for side in (0, 1):
+        lo = o.iterate(side)
+        ld = c.wals_half(side, ALPHA, lam) / (o.nusers * o.nitems)
+        assert rel_err(c.factors(side), o.factors(side)) < tol, side
+        assert abs(ld - lo) < tol * abs(lo) * 10
+        c.set_factors(side, o.factors(side))  # lock-step: each half checked on its own
