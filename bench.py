@@ -26,6 +26,8 @@ CONFIGS = {
     "c3": (10_000_000, 1_000_000, 500_000_000, 128, 3),
     "c2": (1_000_000, 100_000, 50_000_000, 64, 2),
     "small": (200_000, 50_000, 10_000_000, 128, 5),
+    # C3's matrix at k = 256 (multi-wave row kernel)
+    "c5": (10_000_000, 1_000_000, 500_000_000, 256, 3),
     # BPR: C2's matrix, k=64, 3 negatives, lr 0.05, no biases
     "c4": (1_000_000, 100_000, 50_000_000, 64, 2),
 }
@@ -93,6 +95,7 @@ def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
 # kernels of each timed class (names as rocprofv3 reports them)
 CLASS_KERNELS = {
     "wals_direct_kernel": ("wals_direct_kernel<",),
+    "wals_big_kernel": ("wals_big_kernel<",),
     "wals_whitened (row solve + unwhiten)": ("wals_woodbury_kernel<", "whiten_kernel<{T}, {NT}, true>"),
 }
 
@@ -275,7 +278,8 @@ def main():
     peak_tf = PEAK_F32_TFLOPS if args.precision == 32 else PEAK_F64_TFLOPS
     ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
     classes = {}
-    for cls, name in ((0, "wals_direct_kernel"), (1, "wals_whitened (row solve + unwhiten)")):
+    direct_name = "wals_big_kernel" if (k > 128 if args.precision == 32 else k > 64) else "wals_direct_kernel"
+    for cls, name in ((0, direct_name), (1, "wals_whitened (row solve + unwhiten)")):
         ks = ctx.kernel_stats(cls)
         if ks["launches"] == 0 or ks["ms"] <= 0:
             continue
