@@ -70,7 +70,10 @@ def test_ml100k_bit_exact_with_mkl_dsysv(tmp_path):
         "o.set_factors(1,d['init'][:o.nitems*30].reshape(o.nitems,30)); o.optimize(10,4)\n"
         "print(md5(factor_text(o.ids(0),o.factors(0))), md5(factor_text(o.ids(1),o.factors(1))))\n"
     ) % (os.path.join(os.path.dirname(__file__), "..", "oracle"), os.path.dirname(__file__))
-    env = dict(os.environ, ORC_LAPACK=str(libdir / "libmkl_rt.so.1"),
+    # MKL picks a code path per host CPU; the md5s were recorded on a host whose path rounds
+    # like MKL's conditional-numerical-reproducibility "COMPATIBLE" branch, so pin that branch
+    # (without it the user file differs in last digits on AVX-512 hosts).
+    env = dict(os.environ, ORC_LAPACK=str(libdir / "libmkl_rt.so.1"), MKL_CBWR="COMPATIBLE",
                MKL_THREADING_LAYER="SEQUENTIAL", LD_LIBRARY_PATH=str(libdir))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                          timeout=300)
