@@ -522,28 +522,55 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   const bool isP = mine && wl > T(0);
   const bool isQ = mine && wl == T(0);
   int bad = __any(mine && wl < T(0)) ? 1 : 0;  // negative confidence: not SPD in this form
-  const bool hasQ = __any(isQ);
+  const uint64_t mQ = __ballot(isQ);
+  const bool hasQ = mQ != 0;
 
-  // gather Zₛ into registers: zr[I][q] = z_{16I+cl}[16q + 4kk .. +3]
+  // gather Zₛ into registers: zr[I][q] = z_{16I+cl}[16q + 4kk .. +3].  Padding signals
+  // (e ≥ n, cr = 0) load row 0: their K rows/columns are replaced by the identity below and
+  // their u and c are 0, so the values never reach a result.
   v4 zr[NTN][NTK];
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
-    const int e = 16 * I + cl;
-    const int ce = __shfl(cr, e, 64);
-    const bool ve = e < n;
-    const v4* zrow = reinterpret_cast<const v4*>(a.Y + (int64_t)ce * KP) + kk;
+    const int ce = __shfl(cr, 16 * I + cl, 64);
+    const v4* zrow = reinterpret_cast<const v4*>(a.Y + (uint64_t)(uint32_t)ce * KP) + kk;
 #pragma unroll
-    for (int q = 0; q < NTK; ++q) {
-      const v4 z = zrow[4 * q];
-      zr[I][q] = ve ? z : v4{0, 0, 0, 0};
-    }
+    for (int q = 0; q < NTK; ++q) zr[I][q] = zrow[4 * q];
   }
   // K = Zₛ Zₛᵀ (lower tiles); the summation index j = 16q + 4kk + comp is the same for the
   // A and B operands, so its order within a step does not matter
   acc_t acc[NTT];
 #pragma unroll
   for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
-  if (!(a.ablate & 16)) {
+  if (a.ablate & 16) {
+  } else if constexpr (sizeof(T) == 4) {
+    // fp32: 32-deep chunks on the bf16 matrix cores, exact 3-way split (see split3):
+    // chunk s takes the lane's columns q = 2s, 2s+1 (8 values) as its k-slice
+    constexpr int NS = (NTK + 1) / 2;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      Split3 sp[NTN];
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        float x[8];
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          x[c4] = zr[I][2 * s][c4];
+          x[4 + c4] = (2 * s + 1 < NTK) ? zr[I][(2 * s + 1) % NTK][c4] : 0.f;
+        }
+        split3(x, sp[I]);
+      }
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+          acc[t] = mma_split6(sp[I], sp[J], acc[t]);
+        }
+      }
+      // one chunk's splits live at a time (keeps the NTN = 3 kernel at 3 waves/SIMD)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
 #pragma unroll
     for (int q = 0; q < NTK; ++q) {
 #pragma unroll
@@ -569,7 +596,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
       for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = T(0);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      const bool qe = __shfl((int)isQ, 16 * I + cl, 64) != 0;
+      const bool qe = (mQ >> (16 * I + cl)) & 1;
 #pragma unroll
       for (int q = 0; q < NTK; ++q)
 #pragma unroll
@@ -597,20 +624,22 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   }
   // S = W_P⁻¹ + K_PP on P×P, identity elsewhere (Q rows and padding)
   const T iw = isP ? fast_rcp(wl) : T(0);
+  const uint64_t mP = __ballot(isP);
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
+    // the diagonal element (e, e), e = 16I + cl, sits in this lane's column cl
+    const T iwd = __shfl(iw, 16 * I + cl, 64);
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
       const int t = tile_index(I, J);
       const int f = 16 * J + cl;
-      const bool pf = __shfl((int)isP, f, 64) != 0;
+      const bool pf = (mP >> f) & 1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int e = 16 * I + M::crow(lane, r);
-        const bool pe = __shfl((int)isP, e, 64) != 0;
-        const T iwe = __shfl(iw, e, 64);
+        const bool pe = (mP >> e) & 1;
         T v = acc[t][r];
-        if (pe && pf) v += (e == f) ? iwe : T(0);
+        if (pe && pf) v += (e == f) ? iwd : T(0);
         else v = (e == f) ? T(1) : T(0);
         acc[t][r] = v;
       }
@@ -624,8 +653,8 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
     const int e = 16 * I + cl;
-    const bool pe = __shfl((int)isP, e, 64) != 0;
-    const bool qe = __shfl((int)isQ, e, 64) != 0;
+    const bool pe = (mP >> e) & 1;
+    const bool qe = (mQ >> e) & 1;
     ul[I] = pe ? S.xs[e] : (qe ? T(1) : T(0));
     cv[I] = __shfl(cwl, e, 64);
   }
