@@ -13,6 +13,16 @@ __device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sq
 __device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
+// Pivot of a Cholesky column: l = √d and 1/l.  fp32: one v_rsq_f32 on the critical path
+// (l = d·(1/√d)); fp64: correctly rounded √d and an exact division.
+__device__ __forceinline__ void pivot_sqrt(float d, float& l, float& inv) {
+  inv = __builtin_amdgcn_rsqf(d);
+  l = d * inv;
+}
+__device__ __forceinline__ void pivot_sqrt(double d, double& l, double& inv) {
+  l = sqrt(d);
+  inv = 1.0 / l;
+}
 
 // Sum over the 16 lanes of a DPP row (lanes 16g..16g+15); every lane receives the sum.
 __device__ __forceinline__ float row16_sum(float v) {

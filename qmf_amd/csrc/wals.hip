@@ -137,41 +137,55 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
       for (int c = 0; c < 16; ++c) pa[s][c] = S.panel[qq * PLD + c];
       pb[s] = S.bw[16 * p + qq];
     }
+    // lanes 0..15 collect the panel's 1/L[c][c] and y_c (lane c), stored once per panel
+    T invv = T(0), yv = T(0);
     if (!(ablate & 2)) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
+        // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the
+        // update below uses L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]
+        T am[16];
+#pragma unroll
+        for (int m = c + 1; m < 16; ++m) am[m] = readlane(pa[0][c], m);
         const T d = readlane(pa[0][c], c);
+        const T bc = readlane(pb[0], c);
         bad |= !(d > T(0));
-        const T ljj = fast_sqrt(d);
-        const T inv = fast_rcp(ljj);
-        if (lane == 0) S.invd[16 * p + c] = inv;
-        // lq = L[q][c] below the diagonal, 0 elsewhere: the updates are unconditional FMAs
-        T lq[SLOTS];
+        T ljj, inv;
+        pivot_sqrt(d, ljj, inv);
+        if (lane == c) {
+          invv = inv;
+          yv = bc * inv;
+        }
+        // lqs = L[q][c]/L[c][c] below the diagonal, 0 elsewhere: the updates are
+        // unconditional FMAs
+        T lqs[SLOTS];
 #pragma unroll
         for (int s = 0; s < SLOTS; ++s) {
-          lq[s] = T(0);
+          lqs[s] = T(0);
           if (64 * s < R) {
             const int q = lane + 64 * s;
-            lq[s] = q > c ? pa[s][c] * inv : T(0);
-            pa[s][c] = q > c ? lq[s] : (q == c ? ljj : pa[s][c]);
+            const T lq = pa[s][c] * inv;
+            lqs[s] = q > c ? lq * inv : T(0);
+            pa[s][c] = q > c ? lq : (q == c ? ljj : pa[s][c]);
           }
         }
-        const T yc = readlane(pb[0], c) * inv;
-        if (lane == 0) S.bw[16 * p + c] = yc;
 #pragma unroll
         for (int s = 0; s < SLOTS; ++s)
-          if (64 * s < R) pb[s] -= lq[s] * yc;
+          if (64 * s < R) pb[s] -= lqs[s] * bc;
 #pragma unroll
         for (int m = c + 1; m < 16; ++m) {
-          const T lm = readlane(lq[0], m);
 #pragma unroll
           for (int s = 0; s < SLOTS; ++s)
-            if (64 * s < R) pa[s][m] -= lq[s] * lm;
+            if (64 * s < R) pa[s][m] -= lqs[s] * am[m];
         }
         // one column per scheduling window: hoisting readlanes across columns blows the
         // SGPR budget
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
+    if (lane < 16) {
+      S.invd[16 * p + lane] = invv;
+      S.bw[16 * p + lane] = yv;
     }
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
