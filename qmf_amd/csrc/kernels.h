@@ -5,6 +5,15 @@
 
 namespace qmfx {
 
+// Per-slot row descriptor of a side's processing order (built once with the buckets):
+// the CSR range of the row and the row itself, so a persistent row kernel reaches a row's
+// signals in one dependent load instead of order → rowptr → signals.
+struct RowDesc {
+  int64_t beg;
+  int32_t n;
+  int32_t row;
+};
+
 template <typename T>
 struct SolveArgs {
   const int64_t* rowptr;  // CSR of the side being solved
@@ -23,7 +32,14 @@ struct SolveArgs {
   int k;                  // real number of factors (≤ KP)
   int ablate;             // timing experiments only: bit0 skip Gram loop, bit1 skip panel
                           // factorization, bit2 skip trailing MFMA update, bit3 skip backward
+  const RowDesc* desc;    // per-slot descriptors (persistent row kernels; indexed like order)
+  const T* Gimg;          // direct kernel: G + λI as per-lane accumulator tiles (gimg_kernel)
+  uint64_t* trace;        // diagnostics only (QMFX_TRACE): per-slot phase timestamps
 };
+
+// G + λI (padding diagonal 1) → the direct row kernel's accumulator-tile image
+hipError_t launch_gimg(const float* G, int nt, int k, double lambda, float* img, hipStream_t s);
+hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* img, hipStream_t s);
 
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s);

@@ -54,6 +54,7 @@ struct SideBuf {
   // direct rows, heaviest first].  wb[i]..wb[i+1] = whitened bucket NTN = i+1; wb[4]..n_ord
   // = direct.  nnz per bucket class for the roofline accounting.
   int64_t* d_order = nullptr;
+  RowDesc* d_desc = nullptr;  // per slot of d_order: CSR range and row
   int64_t wb[5] = {0, 0, 0, 0, 0};
   int64_t n_ord = 0;
   double nnz_w = 0, nnz_d = 0;
@@ -106,6 +107,9 @@ struct qmfx_ctx {
   int64_t z_cap = 0;
   void* Linv = nullptr;  // kp × kp
   int32_t* chol_status = nullptr;
+  void* Gimg = nullptr;  // G + λI as the direct kernel's accumulator-tile image
+  uint64_t* trace = nullptr;  // QMFX_TRACE diagnostics: whitened-row phase timestamps
+  int64_t trace_cap = 0;
   // per-class timing: 0 direct kernel, 1 whitened kernels (row solve + unwhiten), 2 whole half
   hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};
   double cls_ms[3] = {0, 0, 0}, cls_flops[3] = {0, 0, 0}, cls_bytes[3] = {0, 0, 0};
@@ -206,6 +210,7 @@ int build_buckets(qmfx_ctx* c, int side) {
   SideBuf& sb = c->s[side];
   sb.buckets_valid = false;
   if (sb.h_rowptr.empty()) return 0;
+  if (sb.n > INT32_MAX) return fail("more than 2^31 rows on one side are not supported");
   const int mx = max_whitened_ntn(c);
   std::vector<int64_t> wlist[4];
   std::vector<std::pair<int64_t, int64_t>> direct;
@@ -243,6 +248,15 @@ int build_buckets(qmfx_ctx* c, int side) {
   sb.d_order = nullptr;
   HIPCHK(hipMalloc(&sb.d_order, (size_t)std::max<int64_t>(sb.n_ord, 1) * 8));
   HIPCHK(scopy(c, sb.d_order, order.data(), (size_t)sb.n_ord * 8, hipMemcpyHostToDevice));
+  std::vector<RowDesc> desc((size_t)sb.n_ord);
+  for (size_t i = 0; i < desc.size(); ++i) {
+    const int64_t r = order[i];
+    desc[i] = RowDesc{sb.h_rowptr[r], (int32_t)(sb.h_rowptr[r + 1] - sb.h_rowptr[r]), (int32_t)r};
+  }
+  if (sb.d_desc) (void)hipFree(sb.d_desc);
+  sb.d_desc = nullptr;
+  HIPCHK(hipMalloc(&sb.d_desc, (size_t)std::max<int64_t>(sb.n_ord, 1) * sizeof(RowDesc)));
+  HIPCHK(scopy(c, sb.d_desc, desc.data(), desc.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
   sb.buckets_valid = true;
   return 0;
 }
@@ -288,6 +302,7 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->evh[i]);
   if (e == hipSuccess) e = hipMalloc(&c->Linv, (size_t)c->kp * c->kp * c->esz);
+  if (e == hipSuccess) e = hipMalloc(&c->Gimg, (size_t)(nt * (nt + 1) / 2) * 256 * c->esz);
   if (e == hipSuccess) e = hipMalloc(&c->chol_status, sizeof(int32_t));
   if (e != hipSuccess) {
     g_err = std::string("qmfx_create: ") + hipGetErrorString(e);
@@ -309,6 +324,7 @@ int qmfx_destroy(qmfx_ctx* c) {
     dfree(sb.val);
     dfree(sb.F);
     dfree_t(sb.d_order);
+    dfree_t(sb.d_desc);
   }
   dfree(c->G);
   dfree_t(c->gpart);
@@ -331,6 +347,8 @@ int qmfx_destroy(qmfx_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   dfree(c->Z);
   dfree(c->Linv);
+  dfree(c->Gimg);
+  dfree_t(c->trace);
   dfree_t(c->chol_status);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -573,6 +591,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            (const double*)c->Linv, nullptr, 0.0, false, c->stream));
     }
   }
+  if (!big) {
+    if (fp32)
+      HIPCHK(launch_gimg((const float*)c->G, c->nt, c->k, lambda, (float*)c->Gimg, c->stream));
+    else
+      HIPCHK(launch_gimg((const double*)c->G, c->nt, c->k, lambda, (double*)c->Gimg, c->stream));
+  }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
   // direct rows (heaviest first)
   HIPCHK(hipEventRecord(c->ev0, c->stream));
@@ -580,16 +604,23 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   if (fp32) {
     SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
                        (float*)L.F, c->rowloss, c->status, L.d_order, d_begin, nD,
-                       (float)alpha, (float)lambda, c->k, c->ablate};
+                       (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, (const float*)c->Gimg};
     HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   } else {
     SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
                         (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
-                        d_begin, nD, alpha, lambda, c->k, c->ablate};
+                        d_begin, nD, alpha, lambda, c->k, c->ablate, L.d_desc,
+                        (const double*)c->Gimg};
     HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
+  const char* trace_path = std::getenv("QMFX_TRACE");
+  if (trace_path && use_w && c->trace_cap < L.n_ord) {
+    dfree_t(c->trace);
+    HIPCHK(hipMalloc(&c->trace, (size_t)L.n_ord * 64));
+    c->trace_cap = L.n_ord;
+  }
   if (use_w) {
     for (int b = 0; b < 4; ++b) {
       const int64_t cnt = L.wb[b + 1] - L.wb[b];
@@ -597,12 +628,13 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
       if (fp32) {
         SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
                            (float*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
-                           (float)alpha, (float)lambda, c->k, c->ablate};
+                           (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
+                           trace_path ? c->trace : nullptr};
         HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       } else {
         SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z, nullptr,
                             (double*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
-                            alpha, lambda, c->k, c->ablate};
+                            alpha, lambda, c->k, c->ablate, L.d_desc, nullptr};
         HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       }
     }
@@ -614,6 +646,15 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
   }
   HIPCHK(hipEventRecord(c->evh[1], c->stream));
+  if (trace_path && use_w) {
+    std::vector<uint64_t> h((size_t)L.wb[4] * 8);
+    HIPCHK(scopy(c, h.data(), c->trace, h.size() * 8, hipMemcpyDeviceToHost));
+    const std::string fn = std::string(trace_path) + "_side" + std::to_string(side) + ".bin";
+    if (FILE* f = std::fopen(fn.c_str(), "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
   HIPCHK(launch_sum_f64(c->rowloss + rb, nrows, c->dsum, c->stream));
   if (c->comm && c->world > 1) {
     NCCLCHK(ncclGroupStart());

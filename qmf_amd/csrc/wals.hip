@@ -21,11 +21,23 @@
 // Data layout in HBM: factors row-major [n][KP], KP = 16·NT ≥ k, zero padding columns;
 // interactions CSR (int64 rowptr, int32 column, value v).  The padded part of every system
 // is the identity, so padded solution entries are exactly zero.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "rowsolve.h"
 
 namespace qmfx {
+
+// threadIdx.x through an asm barrier: lane-derived constants of a persistent kernel's row
+// loop are then recomputed per row instead of being hoisted out of the loop (which turns
+// dozens of lane masks into long-lived SGPRs and spills).
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x));
+  return l;
+}
 
 
 // ---------------------------------------------------------------------------------------
@@ -85,22 +97,57 @@ __device__ __forceinline__ f32x4 mma_split6(const Split3& a, const Split3& b, f3
 //   In:  acc = lower 16×16 tiles of an SPD matrix of size 16·NT (diagonal tiles full);
 //        S.bw = right-hand side (written and synchronised by the caller).
 //   Out: S.xs = solution; S.bw = L⁻¹ b.  `bad` set on a non-positive pivot.
-// Right-looking over 16-column panels: a panel is factored with its rows spread over the
-// lanes (column steps broadcast by readlane), the forward solve riding along as one more
-// register per row; the trailing update A(I,J) −= L(I,p)L(J,p)ᵀ is 4 MFMAs per tile with
-// operands staged through LDS; off-diagonal L tiles return to the registers, diagonal
-// ones to LDS.  Backward solve by 16-blocks: off-diagonal part from the register tiles
-// with a cross-lane reduction, the diagonal triangle by a 16-step substitution with the
-// tile's columns in lanes.
+// Right-looking over 16-column panels.  A panel is factored with its rows spread over the
+// lanes: per column one broadcast (readlane) of the diagonal block's column, issued
+// before the pivot is known, and unconditional FMAs (rows above the pivot only touch
+// their dead upper part); the forward solve rides along as one more register per row.
+// The trailing update A(I,J) −= L(I,p)L(J,p)ᵀ is 4 MFMAs per tile with operands staged
+// through LDS; off-diagonal L tiles return to the registers.  The diagonal L blocks go to
+// LDS transposed and column-scaled, Lt[q][c] = L[c][q]/L[q][q] (q < c, 0 elsewhere), so
+// the backward substitution is one readlane + one FMA per column.
 // ---------------------------------------------------------------------------------------
+template <typename T>
+struct CholLd {
+  // padded LDS row of a panel: fp32 rows are 16-B aligned and conflict-free for the
+  // b128 row accesses and the MFMA-layout tile accesses used here
+  static constexpr int PLD = sizeof(T) == 4 ? 20 : 17;
+};
+
 template <typename T, int NT>
 struct CholShared {
-  T panel[16 * NT * 17];
-  T Ldiag[NT * 16 * 17];
+  static constexpr int PLD = CholLd<T>::PLD;
+  T panel[16 * NT * PLD];
+  T Lt[NT * 16 * PLD];
   T bw[16 * NT];
   T xs[16 * NT];
   T invd[16 * NT];
 };
+
+// 16 consecutive values of an LDS row (b128 accesses for fp32)
+template <typename T>
+__device__ __forceinline__ void lds_row_load(const T* src, T (&v)[16]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 x = reinterpret_cast<const f32x4*>(src)[j];
+      v[4 * j] = x[0], v[4 * j + 1] = x[1], v[4 * j + 2] = x[2], v[4 * j + 3] = x[3];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = src[j];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void lds_row_store(T* dst, const T (&v)[16]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      reinterpret_cast<f32x4*>(dst)[j] = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dst[j] = v[j];
+  }
+}
 
 template <typename T, int NT>
 __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
@@ -109,22 +156,18 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
   using M = Mfma<T>;
   constexpr int KP = 16 * NT;
   constexpr int SLOTS = (KP + 63) / 64;
-  constexpr int PLD = 17;
+  constexpr int PLD = CholShared<T, NT>::PLD;
   const int cl = lane & 15;
   const int kk = lane >> 4;
+#pragma unroll
   for (int p = 0; p < NT; ++p) {
     const int R = KP - 16 * p;
 #pragma unroll
-    for (int I = 0; I < NT; ++I) {
+    for (int I = p; I < NT; ++I) {
+      const int t = tile_index(I, p);
 #pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        if (J == p) {
-          const int t = tile_index(I, J);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[t][r];
-        }
-      }
+      for (int r = 0; r < 4; ++r)
+        S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[t][r];
     }
     __syncthreads();
     T pa[SLOTS][16];
@@ -133,8 +176,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     for (int s = 0; s < SLOTS; ++s) {
       const int q = lane + 64 * s;
       const int qq = q < R ? q : 0;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) pa[s][c] = S.panel[qq * PLD + c];
+      lds_row_load(&S.panel[qq * PLD], pa[s]);
       pb[s] = S.bw[16 * p + qq];
     }
     // lanes 0..15 collect the panel's 1/L[c][c] and y_c (lane c), stored once per panel
@@ -143,46 +185,36 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the
-        // update below uses L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]
+        // update uses L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]
         T am[16];
 #pragma unroll
         for (int m = c + 1; m < 16; ++m) am[m] = readlane(pa[0][c], m);
         const T d = readlane(pa[0][c], c);
         const T bc = readlane(pb[0], c);
-        bad |= !(d > T(0));
         T ljj, inv;
         pivot_sqrt(d, ljj, inv);
-        if (lane == c) {
-          invv = inv;
-          yv = bc * inv;
-        }
-        // lqs = L[q][c]/L[c][c] below the diagonal, 0 elsewhere: the updates are
-        // unconditional FMAs
-        T lqs[SLOTS];
+        (void)ljj;
+        const bool me = lane == c;
+        invv = me ? inv : invv;
+        yv = me ? bc * inv : yv;
+        // every row takes lq = A[q][c]/L[c][c]: below the pivot that is L[q][c], at the
+        // pivot √d; rows above only change their dead upper part (and their pb, which is
+        // no longer read: y comes from yv)
 #pragma unroll
         for (int s = 0; s < SLOTS; ++s) {
-          lqs[s] = T(0);
           if (64 * s < R) {
-            const int q = lane + 64 * s;
             const T lq = pa[s][c] * inv;
-            lqs[s] = q > c ? lq * inv : T(0);
-            pa[s][c] = q > c ? lq : (q == c ? ljj : pa[s][c]);
+            const T lqs = lq * inv;
+            pa[s][c] = lq;
+            pb[s] -= lqs * bc;
+#pragma unroll
+            for (int m = c + 1; m < 16; ++m) pa[s][m] -= lqs * am[m];
           }
         }
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s)
-          if (64 * s < R) pb[s] -= lqs[s] * bc;
-#pragma unroll
-        for (int m = c + 1; m < 16; ++m) {
-#pragma unroll
-          for (int s = 0; s < SLOTS; ++s)
-            if (64 * s < R) pa[s][m] -= lqs[s] * am[m];
-        }
-        // one column per scheduling window: hoisting readlanes across columns blows the
-        // SGPR budget
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // a pivot that is not positive (or not finite) leaves 1/√d outside (0, ∞)
+    bad |= __any(lane < 16 && !(invv > T(0) && invv < __builtin_huge_val())) ? 1 : 0;
     if (lane < 16) {
       S.invd[16 * p + lane] = invv;
       S.bw[16 * p + lane] = yv;
@@ -190,46 +222,41 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int q = lane + 64 * s;
-      if (q < R) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[s][c];
-      }
+      if (q < R) lds_row_store(&S.panel[q * PLD], pa[s]);
       if (q >= 16 && q < R) S.bw[16 * p + q] = pb[s];
     }
     __syncthreads();
+    // diagonal block → Lt (transposed, scaled by the column's 1/L[q][q], zero on and above
+    // the diagonal)
     for (int idx = lane; idx < 256; idx += 64) {
       const int r = idx >> 4, c = idx & 15;
-      S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
+      S.Lt[(p * 16 + c) * PLD + r] = c < r ? S.panel[r * PLD + c] * S.invd[16 * p + c] : T(0);
     }
     T fr[NT][4];
 #pragma unroll
-    for (int I = 0; I < NT; ++I) {
-      if (I > p) {
+    for (int I = p + 1; I < NT; ++I) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) fr[I][s] = S.panel[(16 * (I - p) + cl) * PLD + 4 * s + kk];
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) fr[I][s] = T(0);
-      }
+      for (int s = 0; s < 4; ++s) fr[I][s] = S.panel[(16 * (I - p) + cl) * PLD + 4 * s + kk];
     }
 #pragma unroll
-    for (int I = 0; I < NT; ++I) {
+    for (int I = p + 1; I < NT; ++I) {
+      const int t = tile_index(I, p);
 #pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const int t = tile_index(I, J);
-        if (J == p && I > p) {
+      for (int r = 0; r < 4; ++r)
+        acc[t][r] = S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc[t][r] = S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
-        } else if (J > p && !(ablate & 4)) {
+      for (int J = p + 1; J <= I; ++J) {
+        if (ablate & 4) break;
+        const int tj = tile_index(I, J);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc[t] = M::mma(-fr[I][s], fr[J][s], acc[t]);
-        }
+        for (int s = 0; s < 4; ++s) acc[tj] = M::mma(-fr[I][s], fr[J][s], acc[tj]);
       }
     }
     __syncthreads();
   }
-  // backward solve Lᵀ x = y
+  // backward solve Lᵀ x = y by 16-blocks from the bottom: lane cl carries row cl of the
+  // block scaled by its own 1/L[cl][cl]; column c then finishes x_c (readlane) and
+  // removes it from the rows above with the scaled Lt (one FMA)
 #pragma unroll
   for (int I = NT - 1; I >= 0; --I) {
     if (ablate & 8) break;
@@ -242,17 +269,12 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     }
     part += shfl_xor(part, 16);
     part += shfl_xor(part, 32);
-    // lane (cl) holds v[cl] and column cl of L(I,I): lc[c] = L[c][cl]
-    T vm = S.bw[16 * I + cl] - part;
-    T lc[16];
+    T vm = (S.bw[16 * I + cl] - part) * S.invd[16 * I + cl];
+    T lt[16];
+    lds_row_load(&S.Lt[(16 * I + cl) * PLD], lt);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) lc[c] = S.Ldiag[(I * 16 + c) * PLD + cl];
-#pragma unroll
-    for (int c = 15; c >= 0; --c) {
-      const T xc = readlane(vm, c) * S.invd[16 * I + c];
-      if (lane == 0) S.xs[16 * I + c] = xc;
-      if (cl < c) vm -= lc[c] * xc;
-    }
+    for (int c = 15; c >= 0; --c) vm -= lt[c] * readlane(vm, c);
+    if (lane < 16) S.xs[16 * I + lane] = vm;
     __syncthreads();
   }
 }
@@ -376,10 +398,12 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 }
 
 // ---------------------------------------------------------------------------------------
-// Direct row kernel: one wave64 per row.  Gram A = G + λI + Σ w y yᵀ by 16x16x4 MFMAs into
-// the lower tiles held in registers; b = Σ c y and Σc on the side.  A row's (col, v) pairs
-// are fetched 64 at a time with one coalesced load and broadcast per 4-signal step; the
-// gathers of step s+1 are in flight while the MFMAs of step s run.
+// Direct row kernel: one wave64 per row, persistent (each wave walks the slots
+// blockIdx.x, blockIdx.x + gridDim.x, …; the order is heaviest-first, so every wave gets a
+// similar mix).  Gram A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in
+// registers, starting from the tile image of G + λI (gimg_kernel: one coalesced 16-B load
+// per tile and lane); b = Σ c y and Σc on the side.  The next row's descriptor is loaded
+// while this row computes, so a row starts with one dependent load (its signals).
 // ---------------------------------------------------------------------------------------
 #ifndef QMFX_WAVES_NT8
 #define QMFX_WAVES_NT8 1
@@ -396,108 +420,145 @@ void wals_direct_kernel(SolveArgs<T> a) {
   __shared__ __attribute__((aligned(16))) CholShared<T, NT> S;
   __shared__ __attribute__((aligned(16))) T borig[KP];
 
-  const int lane = threadIdx.x;
-  const int cl = lane & 15;
-  const int kk = lane >> 4;
-  const int64_t slot = a.row_begin + blockIdx.x;
-  const int64_t row = a.order ? a.order[slot] : slot;
-  const int64_t beg = a.rowptr[row];
-  const int64_t end = a.rowptr[row + 1];
+  const int64_t stride = gridDim.x;
+  int64_t i = blockIdx.x;
+  if (i >= a.nrows) return;
+  RowDesc dnext = a.desc[a.row_begin + i];
+  for (; i < a.nrows; i += stride) {
+    const int lane = opaque_lane();
+    const int cl = lane & 15;
+    const int kk = lane >> 4;
+    const RowDesc d = dnext;
+    if (i + stride < a.nrows) dnext = a.desc[a.row_begin + i + stride];
+    const int64_t row = d.row;
+    const int64_t beg = d.beg;
+    const int64_t end = beg + d.n;
 
-  acc_t acc[NTT];
-#pragma unroll
-  for (int I = 0; I < NT; ++I) {
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      const int t = tile_index(I, J);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = M::crow(lane, r);
-        // fp32: the virtual (permuted) index space of gram_split_bf16
-        const int pi = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * I + i) : 16 * I + i;
-        const int pj = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * J + cl) : 16 * J + cl;
-        T g = a.G[(int64_t)pi * KP + pj];
-        if (I == J && i == cl) g += (pi < a.k) ? a.lambda : T(1);
-        acc[t][r] = g;
-      }
-    }
-  }
-  T bpart[NT];
-#pragma unroll
-  for (int c = 0; c < NT; ++c) bpart[c] = T(0);
-  double csum = 0.0;
-  int negw = 0;
-  if constexpr (Perm<NT>::template split<T>) {
-    if (!(a.ablate & 1)) gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
-  } else
-  for (int64_t base = beg; base < end && !(a.ablate & 1); base += 64) {
-    const int nst = (int)(end - base < 64 ? end - base : 64);
-    const int cr = lane < nst ? a.col[base + lane] : 0;
-    const T vr = lane < nst ? a.val[base + lane] : T(0);
-    bool valid = kk < nst;
-    T v = __shfl(vr, kk, 64);
-    T yn[NT];
+    acc_t acc[NTT];
     {
-      const T* yrow = a.Y + (int64_t)__shfl(cr, kk, 64) * KP + cl;
+      // buffer loads: the tile offset rides in the scalar offset, so no per-tile address
+      // registers are kept
+      constexpr int AB = (int)sizeof(acc_t);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.Gimg, (short)0, NTT * 64 * AB, 0x00020000);
 #pragma unroll
-      for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
-    }
-    for (int s = 0; 4 * s < nst; ++s) {
-      T yv[NT];
+      for (int t = 0; t < NTT; ++t) {
 #pragma unroll
-      for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
-      const T w = valid ? a.alpha * v : T(0);
-      const T cw = valid ? T(1) + a.alpha * v : T(0);
-      const int jn = 4 * (s + 1) + kk;
-      const bool vn = jn < nst;
-      if (4 * (s + 1) < nst) {
-        const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
-        v = __shfl(vr, jn < 64 ? jn : 0, 64);
-        const T* yrow = a.Y + (int64_t)(vn ? cn : cr) * KP + cl;
-#pragma unroll
-        for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
-      }
-      valid = vn;
-#pragma unroll
-      for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
-      csum += (double)cw;
-#pragma unroll
-      for (int I = 0; I < NT; ++I) {
-#pragma unroll
-        for (int J = 0; J <= I; ++J) {
-          const int t = tile_index(I, J);
-          acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+        for (int h = 0; h < AB / 16; ++h) {
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * AB + 16 * h,
+                                                                t * 64 * AB, 0);
+          if constexpr (sizeof(T) == 4) {
+            acc[t] = __builtin_bit_cast(acc_t, v);
+          } else {
+            const double lo = __builtin_bit_cast(double, (unsigned long long)v[0] |
+                                                             ((unsigned long long)v[1] << 32));
+            const double hi = __builtin_bit_cast(double, (unsigned long long)v[2] |
+                                                             ((unsigned long long)v[3] << 32));
+            acc[t][2 * h] = lo;
+            acc[t][2 * h + 1] = hi;
+          }
         }
       }
     }
-  }
+    T bpart[NT];
 #pragma unroll
-  for (int q = 0; q < NT; ++q) {
-    bpart[q] += shfl_xor(bpart[q], 16);
-    bpart[q] += shfl_xor(bpart[q], 32);
-    if (kk == 0) {
-      borig[16 * q + cl] = bpart[q];
-      S.bw[16 * q + cl] = bpart[q];
+    for (int c = 0; c < NT; ++c) bpart[c] = T(0);
+    double csum = 0.0;
+    int negw = 0;
+    if constexpr (Perm<NT>::template split<T>) {
+      if (!(a.ablate & 1)) gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
+    } else
+    for (int64_t base = beg; base < end && !(a.ablate & 1); base += 64) {
+      const int nst = (int)(end - base < 64 ? end - base : 64);
+      const int cr = lane < nst ? a.col[base + lane] : 0;
+      const T vr = lane < nst ? a.val[base + lane] : T(0);
+      bool valid = kk < nst;
+      T v = __shfl(vr, kk, 64);
+      T yn[NT];
+      {
+        const T* yrow = a.Y + (uint64_t)(uint32_t)__shfl(cr, kk, 64) * KP + cl;
+#pragma unroll
+        for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
+      }
+      for (int s = 0; 4 * s < nst; ++s) {
+        T yv[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
+        const T w = valid ? a.alpha * v : T(0);
+        const T cw = valid ? T(1) + a.alpha * v : T(0);
+        const int jn = 4 * (s + 1) + kk;
+        const bool vn = jn < nst;
+        if (4 * (s + 1) < nst) {
+          const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
+          v = __shfl(vr, jn < 64 ? jn : 0, 64);
+          const T* yrow = a.Y + (uint64_t)(uint32_t)(vn ? cn : cr) * KP + cl;
+#pragma unroll
+          for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
+        }
+        valid = vn;
+#pragma unroll
+        for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
+        csum += (double)cw;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            const int t = tile_index(I, J);
+            acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+          }
+        }
+      }
     }
-  }
-  csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
-  int bad = __any(negw) ? 1 : 0;  // negative weight: solved on the host
-  __syncthreads();
-  chol_solve<T, NT>(acc, S, lane, bad, a.ablate);
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      bpart[q] += shfl_xor(bpart[q], 16);
+      bpart[q] += shfl_xor(bpart[q], 32);
+      if (kk == 0) {
+        borig[16 * q + cl] = bpart[q];
+        S.bw[16 * q + cl] = bpart[q];
+      }
+    }
+    csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
+    int bad = __any(negw) ? 1 : 0;  // split Gram with a negative weight: solved on the host
+    __syncthreads();
+    chol_solve<T, NT>(acc, S, lane, bad, a.ablate);
 
-  double xb = 0.0, xx = 0.0;
-  for (int i = lane; i < KP; i += 64) {
-    const T xi = S.xs[i];
-    a.X[row * KP + (Perm<NT>::template split<T> ? Perm<NT>::phys(i) : i)] = xi;
-    xb += (double)xi * (double)borig[i];
-    xx += (double)xi * (double)xi;
+    double xb = 0.0, xx = 0.0;
+    for (int j = lane; j < KP; j += 64) {
+      const T xj = S.xs[j];
+      a.X[row * KP + (Perm<NT>::template split<T> ? Perm<NT>::phys(j) : j)] = xj;
+      xb += (double)xj * (double)borig[j];
+      xx += (double)xj * (double)xj;
+    }
+    xb = wave_sum(xb);
+    xx = wave_sum(xx);
+    if (lane == 0) {
+      a.rowloss[row] = bad ? 0.0 : csum - xb - (double)a.lambda * xx;
+      if (bad && a.status) a.status[row] = 1;
+    }
+    __syncthreads();  // S and borig are reused by the next row
   }
-  xb = wave_sum(xb);
-  xx = wave_sum(xx);
-  if (lane == 0) {
-    a.rowloss[row] = bad ? 0.0 : csum - xb - (double)a.lambda * xx;
-    if (bad && a.status) a.status[row] = 1;
-  }
+}
+
+// G + λI (padding diagonal: 1) in the direct kernel's accumulator-tile order:
+// img[(t·64 + lane)·4 + r] = acc[t][r] of `lane`, in the kernel's virtual index space.
+template <typename T, int NT>
+__global__ void gimg_kernel(const T* G, int k, double lambda, T* img) {
+  using M = Mfma<T>;
+  constexpr int KP = 16 * NT;
+  constexpr int NTT = NT * (NT + 1) / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NTT * 256) return;
+  const int r = idx & 3, lane = (idx >> 2) & 63, t = idx >> 8;
+  int I = 0;
+  while (tile_index(I + 1, 0) <= t) ++I;
+  const int J = t - tile_index(I, 0);
+  const int i = M::crow(lane, r), cl = lane & 15;
+  const int pi = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * I + i) : 16 * I + i;
+  const int pj = Perm<NT>::template split<T> ? Perm<NT>::phys(16 * J + cl) : 16 * J + cl;
+  double g = (double)G[(int64_t)pi * KP + pj];
+  if (I == J && i == cl) g += (pi < k) ? lambda : 1.0;
+  img[idx] = (T)g;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -519,18 +580,21 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   __shared__ __attribute__((aligned(16))) CholShared<T, NTN> S;
   __shared__ __attribute__((aligned(16))) T gq[16 * NTN];
 
+  // one row per wave: the slot's descriptor, then its signals (lane = signal)
   const int lane = threadIdx.x;
   const int cl = lane & 15;
   const int kk = lane >> 4;
-  const int64_t slot = a.row_begin + blockIdx.x;
-  const int64_t row = a.order ? a.order[slot] : slot;
-  const int64_t beg = a.rowptr[row];
-  const int n = (int)(a.rowptr[row + 1] - beg);  // ≤ 16·NTN by bucketing
+  const int64_t i = blockIdx.x;
+  const RowDesc dn = a.desc[a.row_begin + i];
+  const int64_t row = dn.row;
+  const int n = dn.n;  // ≤ 16·NTN by bucketing
+  uint64_t tr[5] = {0, 0, 0, 0, 0};
+  if (a.trace) tr[0] = __builtin_amdgcn_s_memtime();
 
   // signal e = lane: column, weight, confidence
   const bool mine = lane < n;
-  const int cr = mine ? a.col[beg + lane] : 0;
-  const T vr = mine ? a.val[beg + lane] : T(0);
+  const int cr = mine ? a.col[dn.beg + lane] : 0;
+  const T vr = mine ? a.val[dn.beg + lane] : T(0);
   const T wl = mine ? a.alpha * vr : T(0);
   const T cwl = mine ? T(1) + a.alpha * vr : T(0);
   const bool isP = mine && wl > T(0);
@@ -549,6 +613,10 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     const v4* zrow = reinterpret_cast<const v4*>(a.Y + (uint64_t)(uint32_t)ce * KP) + kk;
 #pragma unroll
     for (int q = 0; q < NTK; ++q) zr[I][q] = zrow[4 * q];
+  }
+  if (a.trace) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[1] = __builtin_amdgcn_s_memtime();
   }
   // K = Zₛ Zₛᵀ (lower tiles); the summation index j = 16q + 4kk + comp is the same for the
   // A and B operands, so its order within a step does not matter
@@ -661,7 +729,9 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   }
   if (lane < 16 * NTN) S.bw[lane] = rhs;
   __syncthreads();
+  if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
   chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
+  if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
   // u_e: solved for P, 1 for Q (c = 1), 0 for padding
   T ul[NTN], cv[NTN];
 #pragma unroll
@@ -672,15 +742,17 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     ul[I] = pe ? S.xs[e] : (qe ? T(1) : T(0));
     cv[I] = __shfl(cwl, e, 64);
   }
-  // x' = Zₛᵀ u and b' = Zₛᵀ c, column j = 16q + 4kk + comp
-  T xp[NTK][4];
+  // x' = Zₛᵀ u and b' = Zₛᵀ c, column j = 16q + 4kk + comp; lane cl == q of each group
+  // stores its 4 columns of x' (a failed row stores x' = 0, so x = 0 and its loss term is
+  // 0; the host re-solves it)
   double xb = 0.0;
 #pragma unroll
   for (int q = 0; q < NTK; ++q) {
+    T xq[4];
 #pragma unroll
     for (int comp = 0; comp < 4; ++comp) {
       if (a.ablate & 32) {
-        xp[q][comp] = zr[0][q][comp];
+        xq[comp] = zr[0][q][comp];
         continue;
       }
       T sx = T(0), sb = T(0);
@@ -689,16 +761,11 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
         sx += zr[I][q][comp] * ul[I];
         sb += zr[I][q][comp] * cv[I];
       }
-      xp[q][comp] = row16_sum(sx);
-      xb += (double)xp[q][comp] * (double)row16_sum(sb);
+      xq[comp] = row16_sum(sx);
+      xb += (double)xq[comp] * (double)row16_sum(sb);
     }
-  }
-  // store x' (lane cl == q of each group writes its 4 columns)
-#pragma unroll
-  for (int q = 0; q < NTK; ++q) {
     if (cl == q) {
-      // a failed row stores x' = 0 (so x = 0 and its loss term is 0); the host re-solves it
-      v4 o = {xp[q][0], xp[q][1], xp[q][2], xp[q][3]};
+      v4 o = {xq[0], xq[1], xq[2], xq[3]};
       if (bad) o = v4{};
       reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
     }
@@ -708,6 +775,18 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   if (lane == 0) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
     if (bad && a.status) a.status[row] = 1;
+  }
+  if (a.trace && lane == 0) {
+    tr[4] = __builtin_amdgcn_s_memtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* o = a.trace + 8 * (a.row_begin + i);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) o[j] = tr[j];
+    o[5] = hw | ((uint64_t)xcc << 32);
+    o[6] = (uint64_t)n;
+    o[7] = (uint64_t)row;
   }
 }
 
@@ -933,28 +1012,62 @@ __global__ void mfma_selftest_kernel(const T* A, const T* B, T* C) {
 // ---------------------------------------------------------------------------------------
 // Host launchers.
 // ---------------------------------------------------------------------------------------
+// Grid of a persistent one-wave row kernel: every resident slot of the device, capped by
+// the rows.  (QMFX_GRID_SCALE, a timing knob, multiplies the resident count.)
+template <typename K>
+static unsigned persistent_grid(K kernel, int64_t nrows) {
+  static int cus = 0;
+  static double scale = 1.0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    if (const char* e = std::getenv("QMFX_GRID_SCALE")) scale = std::atof(e);
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  const int64_t g = (int64_t)((double)per_cu * cus * scale);
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(nrows, g));
+}
+
 template <typename T, int NT>
 static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
-  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
+  if (!a.desc || !a.Gimg) return hipErrorInvalidValue;
+  const unsigned g = persistent_grid(wals_direct_kernel<T, NT>, a.nrows);
+  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3(g), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int NT>
+static hipError_t launch_gimg_nt(const T* G, int k, double lambda, T* img, hipStream_t s) {
+  constexpr int NTT = NT * (NT + 1) / 2;
+  hipLaunchKernelGGL((gimg_kernel<T, NT>), dim3(NTT), dim3(256), 0, s, G, k, lambda, img);
   return hipGetLastError();
 }
 
 template <typename T, int NTK>
 static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
-  const dim3 g((unsigned)a.nrows), b(64);
+  if (!a.desc) return hipErrorInvalidValue;
+  const dim3 b(64);
+#define QMFX_WB(N) \
+  hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N>), dim3((unsigned)a.nrows), b, 0, s, a)
   if (ntn == 1) {
-    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 1>), g, b, 0, s, a);
+    QMFX_WB(1);
   } else if (ntn == 2) {
-    if constexpr (NTK >= 4) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 2>), g, b, 0, s, a);
+    if constexpr (NTK >= 4) QMFX_WB(2);
     else return hipErrorInvalidValue;
   } else if (ntn == 3) {
-    if constexpr (NTK >= 6) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 3>), g, b, 0, s, a);
+    if constexpr (NTK >= 6) QMFX_WB(3);
     else return hipErrorInvalidValue;
   } else if (ntn == 4) {
-    if constexpr (NTK >= 8) hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, 4>), g, b, 0, s, a);
+    if constexpr (NTK >= 8) QMFX_WB(4);
     else return hipErrorInvalidValue;
+#undef QMFX_WB
   } else {
     return hipErrorInvalidValue;
   }
@@ -1021,6 +1134,17 @@ static hipError_t launch_gram_nt(const T* Y, int64_t n, T* G, double* partial,
     default: return hipErrorInvalidValue; \
   }
 
+hipError_t launch_gimg(const float* G, int nt, int k, double lambda, float* img, hipStream_t s) {
+#define CALL(N) launch_gimg_nt<float, N>(G, k, lambda, img, s)
+  QMFX_NT_SWITCH(nt, CALL)
+#undef CALL
+}
+hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* img,
+                       hipStream_t s) {
+#define CALL(N) launch_gimg_nt<double, N>(G, k, lambda, img, s)
+  QMFX_NT_SWITCH64(nt, CALL)
+#undef CALL
+}
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s) {
 #define CALL(N) launch_direct_nt<float, N>(a, s)
   QMFX_NT_SWITCH(nt, CALL)

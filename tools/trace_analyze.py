@@ -1,0 +1,61 @@
+"""Run one C3-shaped user half with QMFX_TRACE and summarise the whitened-row phases:
+per-phase cycle medians by bucket, and how the two waves of each SIMD overlap."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+path = os.path.join(ROOT, "gpurun_out", "trace")
+os.environ["QMFX_TRACE"] = path
+import qmf_amd  # noqa: E402
+
+cfg = [int(x) for x in sys.argv[1:5]] if len(sys.argv) > 4 else [10_000_000, 1_000_000, 500_000_000, 128]
+c = qmf_amd.Context(cfg[3], 32)
+c.gen_synthetic(cfg[0], cfg[1], cfg[2], 3)
+c.fill_uniform(1, 0.01, 103)
+c.wals_half(0, 40.0, 0.05)
+c.wals_half(0, 40.0, 0.05)
+t = np.fromfile(path + "_side0.bin", dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+os.remove(path + "_side0.bin")
+t = t[t[:, 0] > 0]
+ph = np.diff(t[:, 0:5], axis=1)  # load, K+setup, chol, x'+store
+n = t[:, 6]
+print("rows traced", len(t))
+names = ["load", "K+setup", "chol", "x'+store"]
+for lo, hi in ((1, 16), (17, 32), (33, 48), (49, 64)):
+    m = (n >= lo) & (n <= hi)
+    if m.sum() == 0:
+        continue
+    med = np.median(ph[m], axis=0)
+    print(f"n {lo:2d}-{hi:2d}: rows {m.sum():8d}  " +
+          "  ".join(f"{nm} {v:7.0f}" for nm, v in zip(names, med)) + f"  total {med.sum():7.0f} cyc")
+# per-SIMD concurrency: key = (xcc, cu bits, simd)
+hw = t[:, 5]
+key = (hw >> 32) * 4096 + ((hw >> 8) & 0xff) * 4 + ((hw >> 4) & 3)
+order = np.lexsort((t[:, 0], key))
+t, key = t[order], key[order]
+uk, starts = np.unique(key, return_index=True)
+ends = np.r_[starts[1:], len(key)]
+busy2 = load2 = tot = gap = 0
+sample = np.linspace(0, len(uk) - 1, min(len(uk), 400)).astype(int)
+for s_i in sample:
+    a, b = starts[s_i], ends[s_i]
+    seg = t[a:b]
+    lo_, hi_ = seg[:, 0].min(), seg[:, 4].max()
+    T = hi_ - lo_
+    if T <= 0:
+        continue
+    grid = np.zeros(int(T // 64) + 1, dtype=np.int8)   # waves in compute per 64-cycle bin
+    lgrid = np.zeros_like(grid)                          # waves in load phase
+    for r in seg:
+        grid[(r[1] - lo_) // 64:(r[4] - lo_) // 64] += 1
+        lgrid[(r[0] - lo_) // 64:(r[1] - lo_) // 64] += 1
+    tot += len(grid)
+    busy2 += (grid >= 2).sum()
+    load2 += ((grid == 0) & (lgrid >= 1)).sum()
+    gap += ((grid == 0) & (lgrid == 0)).sum()
+print(f"SIMD time with >=2 waves computing {busy2 / tot:.3f}, only loading {load2 / tot:.3f}, "
+      f"idle {gap / tot:.3f}, exactly one computing {1 - (busy2 + load2 + gap) / tot:.3f}")
+print("waves per SIMD (median rows per SIMD):", int(np.median(ends - starts)))
