@@ -35,6 +35,7 @@ struct SolveArgs {
   const RowDesc* desc;    // per-slot descriptors (persistent row kernels; indexed like order)
   const T* Gimg;          // direct kernel: G + λI as per-lane accumulator tiles (gimg_kernel)
   uint64_t* trace;        // diagnostics only (QMFX_TRACE): per-slot phase timestamps
+  int32_t zrow;           // whitened kernel: index of an all-zero row of Y (padding signals)
 };
 
 // G + λI (padding diagonal 1) → the direct row kernel's accumulator-tile image

@@ -573,9 +573,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                              c->gpart_blocks, c->stream));
   if (use_w) {
     if (c->z_cap < R.n) {
+      // one extra all-zero row (index z_cap): the whitened kernel's padding signals
       dfree(c->Z);
       const int64_t cap = std::max(c->s[0].n, c->s[1].n);
-      HIPCHK(hipMalloc(&c->Z, (size_t)cap * c->kp * c->esz));
+      HIPCHK(hipMalloc(&c->Z, (size_t)(cap + 1) * c->kp * c->esz));
+      HIPCHK(hipMemsetAsync((char*)c->Z + (size_t)cap * c->kp * c->esz, 0, (size_t)c->kp * c->esz,
+                            c->stream));
       c->z_cap = cap;
     }
     HIPCHK(hipMemsetAsync(c->chol_status, 0, 4, c->stream));
@@ -629,12 +632,13 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
         SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
                            (float*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
                            (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
-                           trace_path ? c->trace : nullptr};
+                           trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
         HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       } else {
         SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z, nullptr,
                             (double*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
-                            alpha, lambda, c->k, c->ablate, L.d_desc, nullptr};
+                            alpha, lambda, c->k, c->ablate, L.d_desc, nullptr, nullptr,
+                            (int32_t)c->z_cap};
         HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       }
     }

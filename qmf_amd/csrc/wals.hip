@@ -30,14 +30,6 @@
 
 namespace qmfx {
 
-// threadIdx.x through an asm barrier: lane-derived constants of a persistent kernel's row
-// loop are then recomputed per row instead of being hoisted out of the loop (which turns
-// dozens of lane masks into long-lived SGPRs and spills).
-__device__ __forceinline__ int opaque_lane() {
-  int l;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x));
-  return l;
-}
 
 
 // ---------------------------------------------------------------------------------------
@@ -398,12 +390,12 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 }
 
 // ---------------------------------------------------------------------------------------
-// Direct row kernel: one wave64 per row, persistent (each wave walks the slots
-// blockIdx.x, blockIdx.x + gridDim.x, …; the order is heaviest-first, so every wave gets a
-// similar mix).  Gram A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in
-// registers, starting from the tile image of G + λI (gimg_kernel: one coalesced 16-B load
-// per tile and lane); b = Σ c y and Σc on the side.  The next row's descriptor is loaded
-// while this row computes, so a row starts with one dependent load (its signals).
+// Direct row kernel: one wave64 per row (slot order heaviest-first).  Gram
+// A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in registers, starting from
+// the tile image of G + λI (gimg_kernel: one coalesced 16-B load per tile and lane);
+// b = Σ c y and Σc on the side.  (A persistent variant that prefetched the next row's
+// descriptor measured slower: the trace showed the gathers' latency is a small part of a
+// row, and a fixed grid loses the dispatcher's balancing.)
 // ---------------------------------------------------------------------------------------
 #ifndef QMFX_WAVES_NT8
 #define QMFX_WAVES_NT8 1
@@ -420,16 +412,11 @@ void wals_direct_kernel(SolveArgs<T> a) {
   __shared__ __attribute__((aligned(16))) CholShared<T, NT> S;
   __shared__ __attribute__((aligned(16))) T borig[KP];
 
-  const int64_t stride = gridDim.x;
-  int64_t i = blockIdx.x;
-  if (i >= a.nrows) return;
-  RowDesc dnext = a.desc[a.row_begin + i];
-  for (; i < a.nrows; i += stride) {
-    const int lane = opaque_lane();
-    const int cl = lane & 15;
-    const int kk = lane >> 4;
-    const RowDesc d = dnext;
-    if (i + stride < a.nrows) dnext = a.desc[a.row_begin + i + stride];
+  const int lane = threadIdx.x;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  {
+    const RowDesc d = a.desc[a.row_begin + blockIdx.x];
     const int64_t row = d.row;
     const int64_t beg = d.beg;
     const int64_t end = beg + d.n;
@@ -536,7 +523,6 @@ void wals_direct_kernel(SolveArgs<T> a) {
       a.rowloss[row] = bad ? 0.0 : csum - xb - (double)a.lambda * xx;
       if (bad && a.status) a.status[row] = 1;
     }
-    __syncthreads();  // S and borig are reused by the next row
   }
 }
 
@@ -593,7 +579,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
 
   // signal e = lane: column, weight, confidence
   const bool mine = lane < n;
-  const int cr = mine ? a.col[dn.beg + lane] : 0;
+  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
   const T vr = mine ? a.val[dn.beg + lane] : T(0);
   const T wl = mine ? a.alpha * vr : T(0);
   const T cwl = mine ? T(1) + a.alpha * vr : T(0);
@@ -604,8 +590,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   const bool hasQ = mQ != 0;
 
   // gather Zₛ into registers: zr[I][q] = z_{16I+cl}[16q + 4kk .. +3].  Padding signals
-  // (e ≥ n, cr = 0) load row 0: their K rows/columns are replaced by the identity below and
-  // their u and c are 0, so the values never reach a result.
+  // (e ≥ n) load the all-zero row a.zrow, so their K rows and columns are exactly 0.
   v4 zr[NTN][NTK];
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
@@ -668,84 +653,125 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
       }
     }
   }
-  // right-hand side W_P⁻¹ c_P − K_PQ 1_Q  (kq_e = z_eᵀ Σ_{f∈Q} z_f)
-  T rhs = isP ? cwl * fast_rcp(wl) : T(0);
-  if (hasQ) {
-    T gpart[NTK][4];
-#pragma unroll
-    for (int q = 0; q < NTK; ++q)
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = T(0);
-#pragma unroll
-    for (int I = 0; I < NTN; ++I) {
-      const bool qe = (mQ >> (16 * I + cl)) & 1;
-#pragma unroll
-      for (int q = 0; q < NTK; ++q)
-#pragma unroll
-        for (int comp = 0; comp < 4; ++comp)
-          if (qe) gpart[q][comp] += zr[I][q][comp];
-    }
-#pragma unroll
-    for (int q = 0; q < NTK; ++q)
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = row16_sum(gpart[q][comp]);
+  double xb = 0.0;  // xᵀb of the row (= x'ᵀ Zₛᵀc)
+  T ul[NTN];        // u of signal 16I + cl
+  if (!hasQ) {
+    // Every real signal is in P.  S = W⁻¹ + K on all 16·NTN slots: padding slots have
+    // K = 0 (zero rows) and take W⁻¹ = 1, so S is the identity there and u = 0.
+    const T iw = isP ? fast_rcp(wl) : T(1);
+    const T rhs = isP ? cwl * iw : T(0);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      T s = T(0);
+      const T iwd = __shfl(iw, 16 * I + cl, 64);  // diagonal (e, e), e = 16I + cl
+      const int t = tile_index(I, I);
 #pragma unroll
-      for (int q = 0; q < NTK; ++q)
-#pragma unroll
-        for (int comp = 0; comp < 4; ++comp) s += zr[I][q][comp] * gpart[q][comp];
-      s += shfl_xor(s, 16);
-      s += shfl_xor(s, 32);
-      if (kk == 0) gq[16 * I + cl] = s;
+      for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : T(0);
     }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
     __syncthreads();
-    const T kqv = lane < 16 * NTN ? gq[lane] : T(0);
-    if (isP) rhs -= kqv;
-  }
-  // S = W_P⁻¹ + K_PP on P×P, identity elsewhere (Q rows and padding)
-  const T iw = isP ? fast_rcp(wl) : T(0);
-  const uint64_t mP = __ballot(isP);
+    if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
+    chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
+    if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
+    // xᵀb = uᵀK c = cᵀ(r − W⁻¹u) = Σ_e (c_e/w_e)(c_e − u_e)   (S u = r, r = W⁻¹c)
+    const T ue = lane < 16 * NTN ? S.xs[lane] : T(0);
+    xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
 #pragma unroll
-  for (int I = 0; I < NTN; ++I) {
-    // the diagonal element (e, e), e = 16I + cl, sits in this lane's column cl
-    const T iwd = __shfl(iw, 16 * I + cl, 64);
+    for (int I = 0; I < NTN; ++I) ul[I] = S.xs[16 * I + cl];
+  } else {
+    // General row (some signals with v = 0: c = 1, w = 0, the set Q):
+    // (W_P⁻¹ + K_PP) u_P = W_P⁻¹ c_P − K_PQ 1_Q,  u_Q = 1,  kq_e = z_eᵀ Σ_{f∈Q} z_f
+    T rhs = isP ? cwl * fast_rcp(wl) : T(0);
+    {
+      T gpart[NTK][4];
 #pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      const int t = tile_index(I, J);
-      const int f = 16 * J + cl;
-      const bool pf = (mP >> f) & 1;
+      for (int q = 0; q < NTK; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = 16 * I + M::crow(lane, r);
-        const bool pe = (mP >> e) & 1;
-        T v = acc[t][r];
-        if (pe && pf) v += (e == f) ? iwd : T(0);
-        else v = (e == f) ? T(1) : T(0);
-        acc[t][r] = v;
+        for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = T(0);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        const bool qe = (mQ >> (16 * I + cl)) & 1;
+#pragma unroll
+        for (int q = 0; q < NTK; ++q)
+#pragma unroll
+          for (int comp = 0; comp < 4; ++comp)
+            if (qe) gpart[q][comp] += zr[I][q][comp];
+      }
+#pragma unroll
+      for (int q = 0; q < NTK; ++q)
+#pragma unroll
+        for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = row16_sum(gpart[q][comp]);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        T sq = T(0);
+#pragma unroll
+        for (int q = 0; q < NTK; ++q)
+#pragma unroll
+          for (int comp = 0; comp < 4; ++comp) sq += zr[I][q][comp] * gpart[q][comp];
+        sq += shfl_xor(sq, 16);
+        sq += shfl_xor(sq, 32);
+        if (kk == 0) gq[16 * I + cl] = sq;
+      }
+      __syncthreads();
+      const T kqv = lane < 16 * NTN ? gq[lane] : T(0);
+      if (isP) rhs -= kqv;
+    }
+    // S = W_P⁻¹ + K_PP on P×P, identity elsewhere (Q rows and padding)
+    const T iw = isP ? fast_rcp(wl) : T(0);
+    const uint64_t mP = __ballot(isP);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      // the diagonal element (e, e), e = 16I + cl, sits in this lane's column cl
+      const T iwd = __shfl(iw, 16 * I + cl, 64);
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        const int f = 16 * J + cl;
+        const bool pf = (mP >> f) & 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = 16 * I + M::crow(lane, r);
+          const bool pe = (mP >> e) & 1;
+          T v = acc[t][r];
+          if (pe && pf) v += (e == f) ? iwd : T(0);
+          else v = (e == f) ? T(1) : T(0);
+          acc[t][r] = v;
+        }
       }
     }
-  }
-  if (lane < 16 * NTN) S.bw[lane] = rhs;
-  __syncthreads();
-  if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
-  chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
-  if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
-  // u_e: solved for P, 1 for Q (c = 1), 0 for padding
-  T ul[NTN], cv[NTN];
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    __syncthreads();
+    if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
+    chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
+    if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
+    // u_e: solved for P, 1 for Q (c = 1), 0 for padding
+    T cv[NTN];
 #pragma unroll
-  for (int I = 0; I < NTN; ++I) {
-    const int e = 16 * I + cl;
-    const bool pe = (mP >> e) & 1;
-    const bool qe = (mQ >> e) & 1;
-    ul[I] = pe ? S.xs[e] : (qe ? T(1) : T(0));
-    cv[I] = __shfl(cwl, e, 64);
+    for (int I = 0; I < NTN; ++I) {
+      const int e = 16 * I + cl;
+      const bool pe = (mP >> e) & 1;
+      const bool qe = (mQ >> e) & 1;
+      ul[I] = pe ? S.xs[e] : (qe ? T(1) : T(0));
+      cv[I] = __shfl(cwl, e, 64);
+    }
+    // xᵀb = x'ᵀ(Zₛᵀc)
+#pragma unroll
+    for (int q = 0; q < NTK; ++q) {
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) {
+        T sx = T(0), sb = T(0);
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) {
+          sx += zr[I][q][comp] * ul[I];
+          sb += zr[I][q][comp] * cv[I];
+        }
+        xb += (double)row16_sum(sx) * (double)row16_sum(sb);
+      }
+    }
+    xb = wave_sum(cl == 0 ? xb : 0.0);
   }
-  // x' = Zₛᵀ u and b' = Zₛᵀ c, column j = 16q + 4kk + comp; lane cl == q of each group
-  // stores its 4 columns of x' (a failed row stores x' = 0, so x = 0 and its loss term is
-  // 0; the host re-solves it)
-  double xb = 0.0;
+  // x' = Zₛᵀ u, column j = 16q + 4kk + comp; lane cl == q of each group stores its 4
+  // columns (a failed row stores x' = 0, so x = 0 and its loss term is 0; the host
+  // re-solves it)
 #pragma unroll
   for (int q = 0; q < NTK; ++q) {
     T xq[4];
@@ -755,14 +781,10 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
         xq[comp] = zr[0][q][comp];
         continue;
       }
-      T sx = T(0), sb = T(0);
+      T sx = T(0);
 #pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        sx += zr[I][q][comp] * ul[I];
-        sb += zr[I][q][comp] * cv[I];
-      }
+      for (int I = 0; I < NTN; ++I) sx += zr[I][q][comp] * ul[I];
       xq[comp] = row16_sum(sx);
-      xb += (double)xq[comp] * (double)row16_sum(sb);
     }
     if (cl == q) {
       v4 o = {xq[0], xq[1], xq[2], xq[3]};
@@ -770,7 +792,6 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
       reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
     }
   }
-  xb = wave_sum(cl == 0 ? xb : 0.0);
   const double csum = wave_sum((double)cwl);
   if (lane == 0) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
@@ -1012,33 +1033,11 @@ __global__ void mfma_selftest_kernel(const T* A, const T* B, T* C) {
 // ---------------------------------------------------------------------------------------
 // Host launchers.
 // ---------------------------------------------------------------------------------------
-// Grid of a persistent one-wave row kernel: every resident slot of the device, capped by
-// the rows.  (QMFX_GRID_SCALE, a timing knob, multiplies the resident count.)
-template <typename K>
-static unsigned persistent_grid(K kernel, int64_t nrows) {
-  static int cus = 0;
-  static double scale = 1.0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-    if (const char* e = std::getenv("QMFX_GRID_SCALE")) scale = std::atof(e);
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess ||
-      per_cu <= 0)
-    per_cu = 1;
-  const int64_t g = (int64_t)((double)per_cu * cus * scale);
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(nrows, g));
-}
-
 template <typename T, int NT>
 static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc || !a.Gimg) return hipErrorInvalidValue;
-  const unsigned g = persistent_grid(wals_direct_kernel<T, NT>, a.nrows);
-  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3(g), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
