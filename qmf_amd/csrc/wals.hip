@@ -143,8 +143,7 @@ __device__ __forceinline__ void lds_row_store(T* dst, const T (&v)[16]) {
 
 template <typename T, int NT>
 __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
-                                           CholShared<T, NT>& S, int lane, int& bad,
-                                           int ablate) {
+                                           CholShared<T, NT>& S, int lane, int& bad) {
   using M = Mfma<T>;
   constexpr int KP = 16 * NT;
   constexpr int SLOTS = (KP + 63) / 64;
@@ -173,7 +172,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     }
     // lanes 0..15 collect the panel's 1/L[c][c] and y_c (lane c), stored once per panel
     T invv = T(0), yv = T(0);
-    if (!(ablate & 2)) {
+    {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the
@@ -238,7 +237,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
         acc[t][r] = S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
 #pragma unroll
       for (int J = p + 1; J <= I; ++J) {
-        if (ablate & 4) break;
         const int tj = tile_index(I, J);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc[tj] = M::mma(-fr[I][s], fr[J][s], acc[tj]);
@@ -251,7 +249,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
   // removes it from the rows above with the scaled Lt (one FMA)
 #pragma unroll
   for (int I = NT - 1; I >= 0; --I) {
-    if (ablate & 8) break;
     T part = T(0);
 #pragma unroll
     for (int J = I + 1; J < NT; ++J) {
@@ -453,9 +450,9 @@ void wals_direct_kernel(SolveArgs<T> a) {
     double csum = 0.0;
     int negw = 0;
     if constexpr (Perm<NT>::template split<T>) {
-      if (!(a.ablate & 1)) gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
+      gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
     } else
-    for (int64_t base = beg; base < end && !(a.ablate & 1); base += 64) {
+    for (int64_t base = beg; base < end; base += 64) {
       const int nst = (int)(end - base < 64 ? end - base : 64);
       const int cr = lane < nst ? a.col[base + lane] : 0;
       const T vr = lane < nst ? a.val[base + lane] : T(0);
@@ -508,7 +505,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
     csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
     int bad = __any(negw) ? 1 : 0;  // split Gram with a negative weight: solved on the host
     __syncthreads();
-    chol_solve<T, NT>(acc, S, lane, bad, a.ablate);
+    chol_solve<T, NT>(acc, S, lane, bad);
 
     double xb = 0.0, xx = 0.0;
     for (int j = lane; j < KP; j += 64) {
@@ -556,7 +553,7 @@ __global__ void gimg_kernel(const T* G, int k, double lambda, T* img) {
 // and the HBM traffic per signal is one gathered row, as in the direct kernel.
 // Writes x' (whitened); whiten_kernel<UNWHITEN> maps it to x = L⁻ᵀ x' and adds −λ‖x‖².
 // ---------------------------------------------------------------------------------------
-template <typename T, int NTK, int NTN>
+template <typename T, int NTK, int NTN, bool TRACE>
 __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
@@ -575,7 +572,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   const int64_t row = dn.row;
   const int n = dn.n;  // ≤ 16·NTN by bucketing
   uint64_t tr[5] = {0, 0, 0, 0, 0};
-  if (a.trace) tr[0] = __builtin_amdgcn_s_memtime();
+  if (TRACE) tr[0] = __builtin_amdgcn_s_memtime();
 
   // signal e = lane: column, weight, confidence
   const bool mine = lane < n;
@@ -599,7 +596,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
 #pragma unroll
     for (int q = 0; q < NTK; ++q) zr[I][q] = zrow[4 * q];
   }
-  if (a.trace) {
+  if (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     tr[1] = __builtin_amdgcn_s_memtime();
   }
@@ -608,8 +605,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   acc_t acc[NTT];
 #pragma unroll
   for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
-  if (a.ablate & 16) {
-  } else if constexpr (sizeof(T) == 4) {
+  if constexpr (sizeof(T) == 4) {
     // fp32: 32-deep chunks on the bf16 matrix cores, exact 3-way split (see split3):
     // chunk s takes the lane's columns q = 2s, 2s+1 (8 values) as its k-slice
     constexpr int NS = (NTK + 1) / 2;
@@ -669,9 +665,9 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     }
     if (lane < 16 * NTN) S.bw[lane] = rhs;
     __syncthreads();
-    if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
-    chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
-    if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
+    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
+    chol_solve<T, NTN>(acc, S, lane, bad);
+    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
     // xᵀb = uᵀK c = cᵀ(r − W⁻¹u) = Σ_e (c_e/w_e)(c_e − u_e)   (S u = r, r = W⁻¹c)
     const T ue = lane < 16 * NTN ? S.xs[lane] : T(0);
     xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
@@ -740,9 +736,9 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     }
     if (lane < 16 * NTN) S.bw[lane] = rhs;
     __syncthreads();
-    if (a.trace) tr[2] = __builtin_amdgcn_s_memtime();
-    chol_solve<T, NTN>(acc, S, lane, bad, a.ablate);
-    if (a.trace) tr[3] = __builtin_amdgcn_s_memtime();
+    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
+    chol_solve<T, NTN>(acc, S, lane, bad);
+    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
     // u_e: solved for P, 1 for Q (c = 1), 0 for padding
     T cv[NTN];
 #pragma unroll
@@ -777,10 +773,6 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     T xq[4];
 #pragma unroll
     for (int comp = 0; comp < 4; ++comp) {
-      if (a.ablate & 32) {
-        xq[comp] = zr[0][q][comp];
-        continue;
-      }
       T sx = T(0);
 #pragma unroll
       for (int I = 0; I < NTN; ++I) sx += zr[I][q][comp] * ul[I];
@@ -797,7 +789,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
     if (bad && a.status) a.status[row] = 1;
   }
-  if (a.trace && lane == 0) {
+  if (TRACE && lane == 0) {
     tr[4] = __builtin_amdgcn_s_memtime();
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1053,8 +1045,11 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
-#define QMFX_WB(N) \
-  hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N>), dim3((unsigned)a.nrows), b, 0, s, a)
+#define QMFX_WB(N)                                                                            \
+  if (a.trace)                                                                                \
+    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, true>), dim3((unsigned)a.nrows), b, 0, s, a); \
+  else                                                                                        \
+    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, false>), dim3((unsigned)a.nrows), b, 0, s, a)
   if (ntn == 1) {
     QMFX_WB(1);
   } else if (ntn == 2) {
