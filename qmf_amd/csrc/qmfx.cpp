@@ -137,8 +137,9 @@ int ensure_side_factors(qmfx_ctx* c, int side) {
   SideBuf& sb = c->s[side];
   if (sb.F) return 0;
   if (sb.n <= 0) return fail("shape not set (qmfx_set_shape)");
-  HIPCHK(hipMalloc(&sb.F, (size_t)sb.n * c->kp * c->esz));
-  HIPCHK(hipMemsetAsync(sb.F, 0, (size_t)sb.n * c->kp * c->esz, c->stream));
+  // one extra all-zero row (index n): padding signals of the row kernels gather it
+  HIPCHK(hipMalloc(&sb.F, (size_t)(sb.n + 1) * c->kp * c->esz));
+  HIPCHK(hipMemsetAsync(sb.F, 0, (size_t)(sb.n + 1) * c->kp * c->esz, c->stream));
   return 0;
 }
 
@@ -602,28 +603,30 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
   // direct rows (heaviest first)
+  const char* trace_path = std::getenv("QMFX_TRACE");
+  if (trace_path && c->trace_cap < L.n_ord) {
+    dfree_t(c->trace);
+    HIPCHK(hipMalloc(&c->trace, (size_t)L.n_ord * 64));
+    c->trace_cap = L.n_ord;
+  }
+  if (trace_path) HIPCHK(hipMemsetAsync(c->trace, 0, (size_t)L.n_ord * 64, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   const int64_t nD = L.n_ord - d_begin;
   if (fp32) {
     SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
                        (float*)L.F, c->rowloss, c->status, L.d_order, d_begin, nD,
-                       (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, (const float*)c->Gimg};
+                       (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, (const float*)c->Gimg,
+                       trace_path ? c->trace : nullptr, (int32_t)R.n};
     HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   } else {
     SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
                         (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
                         d_begin, nD, alpha, lambda, c->k, c->ablate, L.d_desc,
-                        (const double*)c->Gimg};
+                        (const double*)c->Gimg, nullptr, (int32_t)R.n};
     HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
-  const char* trace_path = std::getenv("QMFX_TRACE");
-  if (trace_path && use_w && c->trace_cap < L.n_ord) {
-    dfree_t(c->trace);
-    HIPCHK(hipMalloc(&c->trace, (size_t)L.n_ord * 64));
-    c->trace_cap = L.n_ord;
-  }
   if (use_w) {
     for (int b = 0; b < 4; ++b) {
       const int64_t cnt = L.wb[b + 1] - L.wb[b];
@@ -650,8 +653,8 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
   }
   HIPCHK(hipEventRecord(c->evh[1], c->stream));
-  if (trace_path && use_w) {
-    std::vector<uint64_t> h((size_t)L.wb[4] * 8);
+  if (trace_path) {
+    std::vector<uint64_t> h((size_t)L.n_ord * 8);
     HIPCHK(scopy(c, h.data(), c->trace, h.size() * 8, hipMemcpyDeviceToHost));
     const std::string fn = std::string(trace_path) + "_side" + std::to_string(side) + ".bin";
     if (FILE* f = std::fopen(fn.c_str(), "wb")) {

@@ -177,9 +177,12 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
       for (int c = 0; c < 16; ++c) {
         // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the
         // update uses L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]
+        // (constant trip counts with a predicate: the loops must unroll fully before c is
+        // known, or the compiler falls back to indexed register access)
         T am[16];
 #pragma unroll
-        for (int m = c + 1; m < 16; ++m) am[m] = readlane(pa[0][c], m);
+        for (int m = 1; m < 16; ++m)
+          if (m > c) am[m] = readlane(pa[0][c], m);
         const T d = readlane(pa[0][c], c);
         const T bc = readlane(pb[0], c);
         T ljj, inv;
@@ -199,9 +202,13 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
             pa[s][c] = lq;
             pb[s] -= lqs * bc;
 #pragma unroll
-            for (int m = c + 1; m < 16; ++m) pa[s][m] -= lqs * am[m];
+            for (int m = 1; m < 16; ++m)
+              if (m > c) pa[s][m] -= lqs * am[m];
           }
         }
+        // one column per scheduling window: readlanes hoisted across columns exhaust the
+        // SGPRs
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // a pivot that is not positive (or not finite) leaves 1/√d outside (0, ∞)
@@ -219,7 +226,9 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     __syncthreads();
     // diagonal block → Lt (transposed, scaled by the column's 1/L[q][q], zero on and above
     // the diagonal)
-    for (int idx = lane; idx < 256; idx += 64) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = lane + 64 * it;
       const int r = idx >> 4, c = idx & 15;
       S.Lt[(p * 16 + c) * PLD + r] = c < r ? S.panel[r * PLD + c] * S.invd[16 * p + c] : T(0);
     }
@@ -287,65 +296,95 @@ struct Perm {
 
 // Direct-row Gram, fp32 on the bf16 matrix cores: 32 signals per step, lane (c, g) owns
 // signals 8g..8g+7 of the step and virtual column c of every block.  Operands are √w·y
-// (w = αv ≥ 0), so A and B are the same split values: A += Σ w y yᵀ.  b = Σ c y and Σc
-// come from the raw rows.  Software pipeline: the column indices of step s+2 and the rows
-// of step s+1 are in flight while step s's MFMAs run.  A negative weight (1 + αv may still
-// be > 0) sets `negw`; the caller flags the row for the host solve.
+// (w = αv ≥ 0), so A and B are the same split values: A += Σ w y yᵀ; b = Σ c y from the
+// raw rows.  The row's (column, value) pairs are staged through LDS 64 at a time (one
+// coalesced load per lane, a chunk ahead), and each lane reads its 8 as two b128 pairs.
+// Signals past the row's end point at the fixed side's all-zero row a.zrow with v = 0,
+// so they add exactly nothing and need no masking.  Σc is summed at staging.  Pipeline:
+// the rows of step s+1 are in flight while step s's MFMAs run.  A negative weight (1 + αv
+// may still be > 0) sets `negw`; the caller flags the row for the host solve.
 template <int NT>
 __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64_t beg,
                                                 int64_t end, f32x4 (&acc)[NT * (NT + 1) / 2],
                                                 float (&bpart)[NT], double& csum, int& negw,
-                                                int lane) {
+                                                int lane, int (&mcol)[2][64],
+                                                float (&mval)[2][64]) {
   constexpr int KP = 16 * NT;
   constexpr int W = Perm<NT>::W;
   constexpr int NG = NT / W;
   using vecW = float __attribute__((ext_vector_type(W)));
   const int c = lane & 15;
   const int g = lane >> 4;
-  // per step: column index and value of the lane's 8 signals, rows as W-vectors
-  int col0[8], col1[8];
-  float val0[8], val1[8];
-  vecW y0[8][NG], y1[8][NG];
-  auto load_meta = [&](int64_t base, int (&col)[8], float (&val)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t e = base + 8 * g + j;
-      const bool ok = e < end;
-      col[j] = ok ? a.col[e] : -1;
-      val[j] = ok ? a.val[e] : 0.f;
-    }
+  const int n = (int)(end - beg);
+  const int nsteps = (n + 31) >> 5;
+  const int nchunks = (n + 63) >> 6;
+  float cs = 0.f;
+  int pc = a.zrow;
+  float pv = 0.f;
+  auto fetch = [&](int ch) {  // this lane's signal of chunk ch → (pc, pv)
+    const int e = 64 * ch + lane;
+    const bool ok = e < n;
+    pc = ok ? a.col[beg + e] : a.zrow;
+    pv = ok ? a.val[beg + e] : 0.f;
+  };
+  auto stage = [&](int ch) {  // (pc, pv) of chunk ch → LDS
+    const bool ok = 64 * ch + lane < n;
+    cs += ok ? 1.f + a.alpha * pv : 0.f;
+    mcol[ch & 1][lane] = pc;
+    mval[ch & 1][lane] = pv;
+  };
+  auto read_meta = [&](int st, int (&col)[8], float (&val)[8]) {
+    const int o = 32 * (st & 1) + 8 * g;
+    const int4 c0 = *reinterpret_cast<const int4*>(&mcol[(st >> 1) & 1][o]);
+    const int4 c1 = *reinterpret_cast<const int4*>(&mcol[(st >> 1) & 1][o + 4]);
+    const float4 v0 = *reinterpret_cast<const float4*>(&mval[(st >> 1) & 1][o]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&mval[(st >> 1) & 1][o + 4]);
+    col[0] = c0.x, col[1] = c0.y, col[2] = c0.z, col[3] = c0.w;
+    col[4] = c1.x, col[5] = c1.y, col[6] = c1.z, col[7] = c1.w;
+    val[0] = v0.x, val[1] = v0.y, val[2] = v0.z, val[3] = v0.w;
+    val[4] = v1.x, val[5] = v1.y, val[6] = v1.z, val[7] = v1.w;
   };
   auto load_rows = [&](const int (&col)[8], vecW (&y)[8][NG]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const vecW* yr = reinterpret_cast<const vecW*>(a.Y + (int64_t)(col[j] < 0 ? 0 : col[j]) * KP) + c;
+      const vecW* yr =
+          reinterpret_cast<const vecW*>(a.Y + (uint64_t)(uint32_t)col[j] * KP) + c;
 #pragma unroll
-      for (int G = 0; G < NG; ++G) {
-        const vecW v = yr[16 * G];
-        y[j][G] = col[j] < 0 ? vecW{} : v;
-      }
+      for (int G = 0; G < NG; ++G) y[j][G] = yr[16 * G];
     }
   };
-  load_meta(beg, col0, val0);
+  if (nsteps == 0) return;
+  // prologue: chunks 0 (and 1) staged, chunk 2 in flight, step 0's rows in flight
+  fetch(0);
+  stage(0);
+  if (nchunks > 1) {
+    fetch(1);
+    stage(1);
+  }
+  if (nchunks > 2) fetch(2);
+  int col0[8], col1[8];
+  float val0[8], val1[8];
+  vecW y0[8][NG], y1[8][NG];
+  read_meta(0, col0, val0);
   load_rows(col0, y0);
-  if (beg + 32 < end) load_meta(beg + 32, col1, val1);
-  float cs = 0.f;
-  for (int64_t base = beg; base < end; base += 32) {
-    const bool more = base + 32 < end;
-    int col2[8];
-    float val2[8];
+  for (int st = 0; st < nsteps; ++st) {
+    const bool more = st + 1 < nsteps;
     if (more) {
-      load_rows(col1, y1);
-      if (base + 64 < end) load_meta(base + 64, col2, val2);
+      if (((st + 1) & 1) == 0) {
+        // step st+1 opens chunk k = (st+1)/2: stage chunk k+1, fetch chunk k+2
+        const int k = (st + 1) >> 1;
+        if (k + 1 < nchunks) stage(k + 1);
+        if (k + 2 < nchunks) fetch(k + 2);
+      }
+      read_meta(st + 1, col1, val1);
     }
     float sw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float w = a.alpha * val0[j];
-      const float cw = col0[j] >= 0 ? 1.f + w : 0.f;
+      const float cw = 1.f + w;
       negw |= w < 0.f;
       sw[j] = fast_sqrt(fabsf(w));
-      cs += cw;
 #pragma unroll
       for (int G = 0; G < NG; ++G)
 #pragma unroll
@@ -362,6 +401,9 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
         split3(x, sp[W * G + m]);
       }
     }
+    // the next step's rows go out once this step's raw rows are consumed (split), so the
+    // two row buffers never coexist with the split operands
+    if (more) load_rows(col1, y1);
 #pragma unroll
     for (int I = 0; I < NT; ++I) {
 #pragma unroll
@@ -373,17 +415,14 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
     if (more) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        col0[j] = col1[j];
         val0[j] = val1[j];
-        col1[j] = col2[j];
-        val1[j] = val2[j];
 #pragma unroll
         for (int G = 0; G < NG; ++G) y0[j][G] = y1[j][G];
       }
     }
   }
-  // each signal's c is held by the 16 lanes of its group: count it once
-  csum += (double)(c == 0 ? cs : 0.f);
+  const double tot = wave_sum((double)cs);
+  csum += lane == 0 ? tot : 0.0;  // the caller sums the cl == 0 lanes
 }
 
 // ---------------------------------------------------------------------------------------
@@ -397,7 +436,7 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_WAVES_NT8
 #define QMFX_WAVES_NT8 1
 #endif
-template <typename T, int NT>
+template <typename T, int NT, bool TRACE>
 __global__ __launch_bounds__(64, Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : 2)
 void wals_direct_kernel(SolveArgs<T> a) {
   // fp32 at NT = 8: the split-bf16 Gram keeps 144 accumulator + 96 operand + 128 row
@@ -408,6 +447,8 @@ void wals_direct_kernel(SolveArgs<T> a) {
   constexpr int NTT = NT * (NT + 1) / 2;
   __shared__ __attribute__((aligned(16))) CholShared<T, NT> S;
   __shared__ __attribute__((aligned(16))) T borig[KP];
+  __shared__ __attribute__((aligned(16))) int mcol[2][64];
+  __shared__ __attribute__((aligned(16))) float mval[2][64];
 
   const int lane = threadIdx.x;
   const int cl = lane & 15;
@@ -417,6 +458,8 @@ void wals_direct_kernel(SolveArgs<T> a) {
     const int64_t row = d.row;
     const int64_t beg = d.beg;
     const int64_t end = beg + d.n;
+    uint64_t tr[5] = {0, 0, 0, 0, 0};
+    if (TRACE) tr[0] = __builtin_amdgcn_s_memtime();
 
     acc_t acc[NTT];
     {
@@ -444,13 +487,17 @@ void wals_direct_kernel(SolveArgs<T> a) {
         }
       }
     }
+    if (TRACE) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tr[1] = __builtin_amdgcn_s_memtime();
+    }
     T bpart[NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c) bpart[c] = T(0);
     double csum = 0.0;
     int negw = 0;
     if constexpr (Perm<NT>::template split<T>) {
-      gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane);
+      gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
     } else
     for (int64_t base = beg; base < end; base += 64) {
       const int nst = (int)(end - base < 64 ? end - base : 64);
@@ -505,7 +552,9 @@ void wals_direct_kernel(SolveArgs<T> a) {
     csum = wave_sum(cl == 0 ? csum : 0.0);  // each k-slot row counted once
     int bad = __any(negw) ? 1 : 0;  // split Gram with a negative weight: solved on the host
     __syncthreads();
+    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
     chol_solve<T, NT>(acc, S, lane, bad);
+    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
 
     double xb = 0.0, xx = 0.0;
     for (int j = lane; j < KP; j += 64) {
@@ -519,6 +568,18 @@ void wals_direct_kernel(SolveArgs<T> a) {
     if (lane == 0) {
       a.rowloss[row] = bad ? 0.0 : csum - xb - (double)a.lambda * xx;
       if (bad && a.status) a.status[row] = 1;
+    }
+    if (TRACE && lane == 0) {
+      tr[4] = __builtin_amdgcn_s_memtime();
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* o = a.trace + 8 * (a.row_begin + blockIdx.x);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) o[j] = tr[j];
+      o[5] = hw | ((uint64_t)xcc << 32);
+      o[6] = (uint64_t)d.n;
+      o[7] = (uint64_t)row;
     }
   }
 }
@@ -1029,7 +1090,10 @@ template <typename T, int NT>
 static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc || !a.Gimg) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((wals_direct_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
+  if (a.trace)
+    hipLaunchKernelGGL((wals_direct_kernel<T, NT, true>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((wals_direct_kernel<T, NT, false>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

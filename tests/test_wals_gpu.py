@@ -189,3 +189,19 @@ def test_large_k_multiwave_rows(k, precision):
         assert rel_err(c.factors(side), o.factors(side)) < tol, side
         assert abs(ld - lo) < tol * abs(lo) * 10
         c.set_factors(side, o.factors(side))  # lock-step: each half checked on its own
+
+
+@pytest.mark.parametrize("k", [96, 128])
+def test_long_rows_fp32_direct(k):
+    """Rows with hundreds of signals on the fp32 direct kernel: the LDS-staged (column,
+    value) chunks of the split-bf16 Gram (prologue, chunk hand-over, ragged last step, zero-row
+    padding) against the oracle, on both halves."""
+    u, i, v = synth(12000, 60, 30000, seed=k)  # ~500 signals per item, ~2.5 per user
+    lam = 5.0  # well-conditioned for fp32 (see test_tiny_half_steps)
+    o, c = make_pair(u, i, v, k, 32, seed=4, lam=lam)
+    for side in (0, 1):
+        lo = o.iterate(side)
+        ld = c.wals_half(side, ALPHA, lam) / (o.nusers * o.nitems)
+        assert rel_err(c.factors(side), o.factors(side)) < 1e-4, side
+        assert abs(ld - lo) < 1e-4 * abs(lo), side
+        c.set_factors(side, o.factors(side))

@@ -1,5 +1,6 @@
-"""Run one C3-shaped user half with QMFX_TRACE and summarise the whitened-row phases:
-per-phase cycle medians by bucket, and how the two waves of each SIMD overlap."""
+"""Run C3-shaped halves with QMFX_TRACE and summarise the row kernels' phases: per-phase
+cycle medians by row length, and how the waves of each SIMD overlap.
+Whitened rows: load, K+setup, chol, x'+store.  Direct rows: G image, Gram, chol, store."""
 import os
 import sys
 
@@ -15,16 +16,19 @@ cfg = [int(x) for x in sys.argv[1:5]] if len(sys.argv) > 4 else [10_000_000, 1_0
 c = qmf_amd.Context(cfg[3], 32)
 c.gen_synthetic(cfg[0], cfg[1], cfg[2], 3)
 c.fill_uniform(1, 0.01, 103)
-c.wals_half(0, 40.0, 0.05)
-c.wals_half(0, 40.0, 0.05)
-t = np.fromfile(path + "_side0.bin", dtype=np.uint64).reshape(-1, 8).astype(np.int64)
-os.remove(path + "_side0.bin")
+side = int(os.environ.get("SIDE", "0"))
+c.fill_uniform(0, 0.01, 104)
+c.wals_half(side, 40.0, 0.05)
+c.wals_half(side, 40.0, 0.05)
+t = np.fromfile(path + "_side%d.bin" % side, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+os.remove(path + "_side%d.bin" % side)
 t = t[t[:, 0] > 0]
 ph = np.diff(t[:, 0:5], axis=1)  # load, K+setup, chol, x'+store
 n = t[:, 6]
 print("rows traced", len(t))
 names = ["load", "K+setup", "chol", "x'+store"]
-for lo, hi in ((1, 16), (17, 32), (33, 48), (49, 64)):
+bins = ((1, 16), (17, 32), (33, 48), (49, 64), (65, 128), (129, 400), (401, 600), (601, 10**9))
+for lo, hi in bins:
     m = (n >= lo) & (n <= hi)
     if m.sum() == 0:
         continue
