@@ -207,7 +207,18 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
           }
         }
         // one column per scheduling window: readlanes hoisted across columns exhaust the
-        // SGPRs
+        // SGPRs.  The fence pins every slot's updates inside the window; without it the
+        // compiler defers the slots past the diagonal block (rows ≥ 64) to the end of the
+        // panel and spills all 15·16 broadcasts (SGPR spill + readlane + s_nop per FMA).
+#pragma unroll
+        for (int s = 1; s < SLOTS; ++s) {
+          if (64 * s < R) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+              if (m >= c) asm volatile("" : "+v"(pa[s][m]));
+            asm volatile("" : "+v"(pb[s]));
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -303,6 +314,12 @@ struct Perm {
 // so they add exactly nothing and need no masking.  Σc is summed at staging.  Pipeline:
 // the rows of step s+1 are in flight while step s's MFMAs run.  A negative weight (1 + αv
 // may still be > 0) sets `negw`; the caller flags the row for the host solve.
+#ifndef QMFX_GRAM_HEAD
+#define QMFX_GRAM_HEAD 100
+#endif
+#ifndef QMFX_GRAM_VALU
+#define QMFX_GRAM_VALU 2
+#endif
 template <int NT>
 __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64_t beg,
                                                 int64_t end, f32x4 (&acc)[NT * (NT + 1) / 2],
@@ -362,64 +379,65 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
     stage(1);
   }
   if (nchunks > 2) fetch(2);
-  int col0[8], col1[8];
-  float val0[8], val1[8];
-  vecW y0[8][NG], y1[8][NG];
-  read_meta(0, col0, val0);
-  load_rows(col0, y0);
-  for (int st = 0; st < nsteps; ++st) {
-    const bool more = st + 1 < nsteps;
-    if (more) {
+  // One step: the next step's rows go out first (into the other buffer, whose rows were
+  // consumed one step ago), then each block is split right before the tiles of its block
+  // row, so the split VALU of block I+1 issues in the free cycles of row I's MFMAs.  The
+  // two buffers swap roles by a 2× unroll (no register copies).
+  auto step = [&](int st, vecW (&yc)[8][NG], float (&vc)[8], vecW (&yn)[8][NG],
+                  float (&vn)[8]) {
+    if (st + 1 < nsteps) {
       if (((st + 1) & 1) == 0) {
         // step st+1 opens chunk k = (st+1)/2: stage chunk k+1, fetch chunk k+2
         const int k = (st + 1) >> 1;
         if (k + 1 < nchunks) stage(k + 1);
         if (k + 2 < nchunks) fetch(k + 2);
       }
-      read_meta(st + 1, col1, val1);
+      int cn[8];
+      read_meta(st + 1, cn, vn);
+      load_rows(cn, yn);
     }
     float sw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float w = a.alpha * val0[j];
+      const float w = a.alpha * vc[j];
       const float cw = 1.f + w;
       negw |= w < 0.f;
       sw[j] = fast_sqrt(fabsf(w));
 #pragma unroll
       for (int G = 0; G < NG; ++G)
 #pragma unroll
-        for (int m = 0; m < W; ++m) bpart[W * G + m] += cw * y0[j][G][m];
+        for (int m = 0; m < W; ++m) bpart[W * G + m] += cw * yc[j][G][m];
     }
     Split3 sp[NT];
 #pragma unroll
-    for (int G = 0; G < NG; ++G) {
-#pragma unroll
-      for (int m = 0; m < W; ++m) {
-        float x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = sw[j] * y0[j][G][m];
-        split3(x, sp[W * G + m]);
-      }
-    }
-    // the next step's rows go out once this step's raw rows are consumed (split), so the
-    // two row buffers never coexist with the split operands
-    if (more) load_rows(col1, y1);
-#pragma unroll
     for (int I = 0; I < NT; ++I) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = sw[j] * yc[j][I / W][I % W];
+      split3(x, sp[I]);
 #pragma unroll
       for (int J = 0; J <= I; ++J) {
         const int t = tile_index(I, J);
         acc[t] = mma_split6(sp[I], sp[J], acc[t]);
       }
     }
-    if (more) {
+    // issue order: the sqrt/rhs VALU and block 0's split up front, then one MFMA and two
+    // VALU at a time (an MFMA holds the vector issue for 8 of its 16 cycles)
+    __builtin_amdgcn_sched_group_barrier(0x2, QMFX_GRAM_HEAD, 0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        val0[j] = val1[j];
-#pragma unroll
-        for (int G = 0; G < NG; ++G) y0[j][G] = y1[j][G];
-      }
+    for (int i = 0; i < 6 * NT * (NT + 1) / 2; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x2, QMFX_GRAM_VALU, 0);
     }
+  };
+  int col0[8];
+  float val0[8], val1[8];
+  vecW y0[8][NG], y1[8][NG];
+  read_meta(0, col0, val0);
+  load_rows(col0, y0);
+  for (int st = 0; st < nsteps; st += 2) {
+    step(st, y0, val0, y1, val1);
+    if (st + 1 < nsteps) step(st + 1, y1, val1, y0, val0);
   }
   const double tot = wave_sum((double)cs);
   csum += lane == 0 ? tot : 0.0;  // the caller sums the cl == 0 lanes

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Timing experiments: build qmf_amd/_build/var_<name>.so = libqmfx with wals.hip compiled
+# under extra -D flags.  usage: tools/build_variant.sh name "-DFOO=1 -DBAR=2"
+set -e
+cd "$(dirname "$0")/../qmf_amd"
+B=_build
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fno-slp-vectorize $2 -c csrc/wals.hip -o $B/var_$1_wals.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $B/var_$1.so $B/var_$1_wals.o $B/wals_big.o $B/bpr.o $B/data.o $B/qmfx.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -f $B/var_$1_wals.o
