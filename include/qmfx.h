@@ -9,7 +9,9 @@
  *   qmf/wals/WALSEngine.cpp:246-264  WALSEngine::computeXtX        -> inside qmfx_wals_half
  *   qmf/wals/WALSEngine.cpp:266-310  WALSEngine::updateFactorsForOne -> inside qmfx_wals_half
  *   qmf/Matrix.cpp:81-96             linearSymmetricSolve (dsysv_) -> inside qmfx_wals_half
- *   qmf/wals/WALSEngine.cpp:130-163  groupSignals (CSR build)      -> qmfx_upload_csr / qmfx_gen_synthetic
+ *   qmf/wals/WALSEngine.cpp:130-163  groupSignals / sortDataset    -> qmfx_group_signals (device
+ *   qmf/utils/IdIndex.cpp:21-31      IdIndex (id -> idx)              sort + CSR build), qmfx_get_ids;
+ *                                                                     qmfx_upload_csr / qmfx_gen_synthetic
  *   qmf/FactorData.h:55-100          FactorData::setFactors        -> qmfx_set_factors / qmfx_fill_uniform
  *   qmf/bpr/BPREngine.cpp:146-220    BPREngine::optimize / update  -> qmfx_bpr_epoch / qmfx_bpr_apply
  *   qmf/bpr/BPREngine.cpp:246-274    BPREngine::evaluate (loss)    -> qmfx_bpr_eval
@@ -54,6 +56,17 @@ int qmfx_get_shape(qmfx_ctx* ctx, int64_t* nusers, int64_t* nitems, int64_t* nnz
 /* CSR of `side`: rowptr[n_side+1], colidx[nnz] = row index on the other side, values[nnz]. */
 int qmfx_upload_csr(qmfx_ctx* ctx, int side, const int64_t* rowptr, const int32_t* colidx,
                     const double* values, int64_t nnz);
+/* Device ingest of raw interactions (WALSEngine::init / groupSignals / sortDataset,
+ * WALSEngine.cpp:37-69, 130-163; IdIndex.cpp:21-31).  `records` holds nnz packed 24-byte
+ * records in the reference's DatasetElem layout (DatasetReader.h:29-33: int64 userId,
+ * int64 itemId, double value), in file order.  Sets the shape (distinct users, items) and
+ * builds both CSR orientations on the device: rows in ascending-id order, entries by
+ * ascending column id, duplicate (u, i) pairs kept in input order.  nnz < 2^31. */
+int qmfx_group_signals(qmfx_ctx* ctx, const void* records, int64_t nnz, int64_t* nusers,
+                       int64_t* nitems);
+/* Ascending distinct ids of `side` (n_side values; idx = position), after
+ * qmfx_group_signals. */
+int qmfx_get_ids(qmfx_ctx* ctx, int side, int64_t* ids);
 /* Device-generated synthetic matrix: ~nnz uniform unique (u, i) pairs,
  * w in 1..5, both orientations built on the device.  *nnz_out = unique pairs kept. */
 int qmfx_gen_synthetic(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t nnz,

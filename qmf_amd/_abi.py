@@ -35,6 +35,8 @@ SIGNATURES = {
     "qmfx_upload_csr": [vp, c_int, P_i64, P_i32, P_f64, c_i64],
     "qmfx_gen_synthetic": [vp, c_i64, c_i64, c_i64, c_u64, P_i64],
     "qmfx_download_csr": [vp, c_int, P_i64, P_i32, P_f32],
+    "qmfx_group_signals": [vp, vp, c_i64, P_i64, P_i64],
+    "qmfx_get_ids": [vp, c_int, P_i64],
     "qmfx_set_factors": [vp, c_int, P_f64],
     "qmfx_get_factors": [vp, c_int, P_f64],
     "qmfx_fill_uniform": [vp, c_int, c_dbl, c_u64],
@@ -168,6 +170,22 @@ class Context:
         _check(lib().qmfx_gen_synthetic(self.h, nusers, nitems, nnz, seed, ctypes.byref(out)))
         self.nusers, self.nitems = nusers, nitems
         return out.value
+
+    def group_signals(self, users, items, values):
+        """Device ingest (qmfx_group_signals) of raw (user id, item id, value) triples in
+        file order; returns (user ids, item ids), ascending."""
+        rec = np.empty(len(users), dtype=np.dtype([("u", "<i8"), ("i", "<i8"), ("v", "<f8")]))
+        rec["u"], rec["i"], rec["v"] = users, items, values
+        nu, ni = c_i64(0), c_i64(0)
+        _check(lib().qmfx_group_signals(self.h, rec.ctypes.data_as(vp), len(rec),
+                                        ctypes.byref(nu), ctypes.byref(ni)))
+        self.nusers, self.nitems = nu.value, ni.value
+        return self.ids(0), self.ids(1)
+
+    def ids(self, side):
+        out = np.empty(self.nusers if side == 0 else self.nitems, np.int64)
+        _check(lib().qmfx_get_ids(self.h, side, _p(out, P_i64)))
+        return out
 
     def shape(self):
         a, b, c = c_i64(), c_i64(), c_i64()

@@ -121,6 +121,19 @@ hipError_t launch_synth_values_any(const uint64_t* keys, int64_t n, uint64_t div
 hipError_t sort_unique_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int64_t* n_out,
                             int end_bit, hipStream_t s);
 hipError_t sort_keys(uint64_t* keys, uint64_t* scratch, int64_t n, int end_bit, hipStream_t s);
+// Device ingest (ingest.hip): packed 24-byte (user id, item id, value) records already on
+// the device → ascending id tables and both CSR orientations (buffers allocated by the
+// callee, owned by the caller; val in the context precision).
+struct IngestOut {
+  int64_t n[2] = {0, 0};                 // distinct users, items
+  int64_t* ids[2] = {nullptr, nullptr};  // ascending ids
+  int64_t* rowptr[2] = {nullptr, nullptr};
+  int32_t* col[2] = {nullptr, nullptr};
+  void* val[2] = {nullptr, nullptr};
+};
+hipError_t group_records(const void* d_records, int64_t n, int prec, IngestOut& out,
+                         hipStream_t s);
+
 hipError_t launch_fill_uniform_f32(float* X, int64_t n, int kp, int k, double bound,
                                    uint64_t seed, hipStream_t s);
 hipError_t launch_fill_uniform_f64(double* X, int64_t n, int kp, int k, double bound,

@@ -48,6 +48,7 @@ struct SideBuf {
   void* val = nullptr;
   void* F = nullptr;
   std::vector<int64_t> h_rowptr;
+  std::vector<int64_t> h_ids;           // ascending ids (only when built by qmfx_group_signals)
   int64_t rbeg = 0, rend = 0;           // rows solved by this rank
   std::vector<int64_t> bounds;          // per-rank row boundaries (world+1)
   // Row buckets of this rank (device list `order`): [whitened n≤16 | ≤32 | ≤48 | ≤64 |
@@ -368,6 +369,7 @@ int qmfx_set_shape(qmfx_ctx* c, int64_t nusers, int64_t nitems) {
   if (set_dev(c)) return -2;
   for (int side = 0; side < 2; ++side) {
     const int64_t n = side == 0 ? nusers : nitems;
+    c->s[side].h_ids.clear();
     if (c->s[side].n != n) {
       dfree(c->s[side].F);
       dfree_t(c->s[side].rowptr);
@@ -392,6 +394,7 @@ int qmfx_upload_csr(qmfx_ctx* c, int side, const int64_t* rowptr, const int32_t*
   if (side != 0 && side != 1) return fail("side must be 0 or 1");
   SideBuf& sb = c->s[side];
   if (sb.n <= 0) return fail("shape not set (qmfx_set_shape)");
+  sb.h_ids.clear();
   const int64_t nother = c->s[1 - side].n;
   if (rowptr[0] != 0 || rowptr[sb.n] != nnz) return fail("rowptr inconsistent with nnz");
   for (int64_t r = 0; r < sb.n; ++r)
@@ -420,6 +423,73 @@ int qmfx_upload_csr(qmfx_ctx* c, int side, const int64_t* rowptr, const int32_t*
   sb.h_rowptr.assign(rowptr, rowptr + sb.n + 1);
   set_default_bounds(sb, c->world, c->rank);
   if (int rc = build_buckets(c, side)) return rc;
+  return 0;
+}
+
+int qmfx_group_signals(qmfx_ctx* c, const void* records, int64_t nnz, int64_t* nusers,
+                       int64_t* nitems) {
+  if (nnz <= 0) return fail("empty dataset");
+  if (nnz > 0x7fffffffll) return fail("device ingest takes at most 2^31-1 interactions");
+  if (set_dev(c)) return -2;
+  void* d_rec = nullptr;
+  HIPCHK(hipMalloc(&d_rec, (size_t)nnz * 24));
+  hipError_t e = scopy(c, d_rec, records, (size_t)nnz * 24, hipMemcpyHostToDevice);
+  IngestOut o;
+  if (e == hipSuccess) e = group_records(d_rec, nnz, c->prec, o, c->stream);
+  (void)hipFree(d_rec);
+  auto release = [&]() {
+    for (int s = 0; s < 2; ++s) {
+      dfree_t(o.ids[s]);
+      dfree_t(o.rowptr[s]);
+      dfree_t(o.col[s]);
+      dfree(o.val[s]);
+    }
+  };
+  if (e != hipSuccess) {
+    release();
+    return fail(std::string("device ingest: ") + hipGetErrorString(e), -2);
+  }
+  if (int rc = qmfx_set_shape(c, o.n[0], o.n[1])) {
+    release();
+    return rc;
+  }
+  for (int side = 0; side < 2; ++side) {
+    SideBuf& sb = c->s[side];
+    dfree_t(sb.rowptr);
+    dfree_t(sb.col);
+    dfree(sb.val);
+    sb.rowptr = o.rowptr[side];
+    sb.col = o.col[side];
+    sb.val = o.val[side];
+    o.rowptr[side] = nullptr;
+    o.col[side] = nullptr;
+    o.val[side] = nullptr;
+    sb.nnz = nnz;
+    sb.h_ids.resize((size_t)sb.n);
+    sb.h_rowptr.resize((size_t)sb.n + 1);
+    e = scopy(c, sb.h_ids.data(), o.ids[side], (size_t)sb.n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+      e = scopy(c, sb.h_rowptr.data(), sb.rowptr, (size_t)(sb.n + 1) * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      release();
+      return fail(std::string("device ingest: ") + hipGetErrorString(e), -2);
+    }
+    set_default_bounds(sb, c->world, c->rank);
+  }
+  release();
+  c->nnz = nnz;
+  for (int side = 0; side < 2; ++side)
+    if (int rc = build_buckets(c, side)) return rc;
+  if (nusers) *nusers = c->s[0].n;
+  if (nitems) *nitems = c->s[1].n;
+  return 0;
+}
+
+int qmfx_get_ids(qmfx_ctx* c, int side, int64_t* ids) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  const SideBuf& sb = c->s[side];
+  if ((int64_t)sb.h_ids.size() != sb.n) return fail("no id table: the CSR was not built by qmfx_group_signals");
+  std::copy(sb.h_ids.begin(), sb.h_ids.end(), ids);
   return 0;
 }
 

@@ -1,5 +1,6 @@
 #include <qmf/wals/WALSEngine.h>
 
+#include <limits>
 #include <random>
 
 #include <qmf/Matrix.h>
@@ -25,8 +26,29 @@ WALSEngine::~WALSEngine() = default;
 void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
   CHECK(!userFactors_ && !itemFactors_) << "engine was already initialized with train data";
   CHECK_GT(config_.nfactors, 0);
-  SignalCsr byUser, byItem;
-  groupSignals(dataset, userIndex_, itemIndex_, byUser, byItem, parallel_.nthreads());
+  CHECK(!dataset.empty()) << "empty train dataset";
+  dev_ = std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors);
+  qmfx_ctx* c = dev_->get();
+  if (dataset.size() < static_cast<size_t>(std::numeric_limits<int32_t>::max())) {
+    // ids, idx and both CSR orientations built on the device (qmfx_group_signals)
+    int64_t nu = 0, ni = 0;
+    QMFX_CHECK(qmfx_group_signals(c, dataset.data(), static_cast<int64_t>(dataset.size()), &nu,
+                                  &ni));
+    std::vector<int64_t> uids(static_cast<size_t>(nu)), iids(static_cast<size_t>(ni));
+    QMFX_CHECK(qmfx_get_ids(c, QMFX_USERS, uids.data()));
+    QMFX_CHECK(qmfx_get_ids(c, QMFX_ITEMS, iids.data()));
+    userIndex_.assignSorted(std::move(uids));
+    itemIndex_.assignSorted(std::move(iids));
+  } else {
+    // beyond the device sort's 32-bit item count: the same grouping on the host
+    SignalCsr byUser, byItem;
+    groupSignals(dataset, userIndex_, itemIndex_, byUser, byItem, parallel_.nthreads());
+    QMFX_CHECK(qmfx_set_shape(c, static_cast<int64_t>(nusers()), static_cast<int64_t>(nitems())));
+    QMFX_CHECK(qmfx_upload_csr(c, QMFX_USERS, byUser.rowptr.data(), byUser.col.data(),
+                               byUser.val.data(), static_cast<int64_t>(byUser.nnz())));
+    QMFX_CHECK(qmfx_upload_csr(c, QMFX_ITEMS, byItem.rowptr.data(), byItem.col.data(),
+                               byItem.val.data(), static_cast<int64_t>(byItem.nnz())));
+  }
 
   userFactors_ = std::make_unique<FactorData>(nusers(), config_.nfactors);
   itemFactors_ = std::make_unique<FactorData>(nitems(), config_.nfactors);
@@ -41,13 +63,6 @@ void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
     itemFactors_->setFactors(config_.DistributionFile);
   }
 
-  dev_ = std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors);
-  qmfx_ctx* c = dev_->get();
-  QMFX_CHECK(qmfx_set_shape(c, static_cast<int64_t>(nusers()), static_cast<int64_t>(nitems())));
-  QMFX_CHECK(qmfx_upload_csr(c, QMFX_USERS, byUser.rowptr.data(), byUser.col.data(),
-                             byUser.val.data(), static_cast<int64_t>(byUser.nnz())));
-  QMFX_CHECK(qmfx_upload_csr(c, QMFX_ITEMS, byItem.rowptr.data(), byItem.col.data(),
-                             byItem.val.data(), static_cast<int64_t>(byItem.nnz())));
   QMFX_CHECK(qmfx_set_factors(c, QMFX_USERS, userFactors_->getFactors().data()));
   QMFX_CHECK(qmfx_set_factors(c, QMFX_ITEMS, itemFactors_->getFactors().data()));
   hostStale_ = false;
