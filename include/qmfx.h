@@ -92,6 +92,8 @@ int qmfx_wals_half(qmfx_ctx* ctx, int side, double alpha, double lambda, double*
  * written to rows[] (up to cap).  The C++ engine re-solves them on the host with an LDLᵀ
  * (Bunch-Kaufman) solve, as dsysv_ would. */
 int qmfx_wals_failed_rows(qmfx_ctx* ctx, int64_t* rows, int64_t cap, int64_t* count);
+/* Per-row loss terms of the last half (n_side values; the sum is *loss_sum). */
+int qmfx_wals_row_losses(qmfx_ctx* ctx, double* out);
 /* Host-side re-solve input for a failed row: A (k×k row-major, λ included) and b. */
 int qmfx_wals_row_system(qmfx_ctx* ctx, int side, int64_t row, double alpha, double lambda,
                          double* A, double* b, double* csum);

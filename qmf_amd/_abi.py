@@ -42,6 +42,7 @@ SIGNATURES = {
     "qmfx_fill_uniform": [vp, c_int, c_dbl, c_u64],
     "qmfx_wals_half": [vp, c_int, c_dbl, c_dbl, P_f64],
     "qmfx_wals_failed_rows": [vp, P_i64, c_i64, P_i64],
+    "qmfx_wals_row_losses": [vp, P_f64],
     "qmfx_wals_row_system": [vp, c_int, c_i64, c_dbl, c_dbl, P_f64, P_f64, P_f64],
     "qmfx_wals_set_row": [vp, c_int, c_i64, P_f64],
     "qmfx_bpr_set_positives": [vp, P_i64, P_i64, c_i64],
@@ -223,6 +224,11 @@ class Context:
         out = c_dbl(0)
         _check(lib().qmfx_wals_half(self.h, side, alpha, lam, ctypes.byref(out)))
         return out.value
+
+    def row_losses(self, side):
+        out = np.empty(self._n(side), np.float64)
+        _check(lib().qmfx_wals_row_losses(self.h, _p(out, P_f64)))
+        return out
 
     def failed_rows(self):
         cnt = c_i64(0)

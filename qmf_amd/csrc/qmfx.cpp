@@ -40,6 +40,8 @@ int fail(const std::string& m, int code = -1) {
     if (r_ != ncclSuccess) return fail(std::string(#x) + ": " + ncclGetErrorString(r_), -3); \
   } while (0)
 
+#define QMFX_MAX_PIECES 16
+
 struct SideBuf {
   int64_t n = 0;
   int64_t nnz = 0;
@@ -61,6 +63,15 @@ struct SideBuf {
   double nnz_w = 0, nnz_d = 0;
   double flops_w = 0;  // algorithmic flops of the whitened rows per half (see qmfx_wals_half)
   bool buckets_valid = false;
+  // Solve pieces: this rank's rows split into nnz-balanced contiguous sub-ranges, each with
+  // its own section of the order list laid out as above (ord + wb[i] relative).  With
+  // several ranks, piece j of every rank is all-gathered while piece j+1 is solved.
+  struct Piece {
+    int64_t rb = 0, re = 0, ord = 0, n_ord = 0;
+    int64_t wb[5] = {0, 0, 0, 0, 0};
+  };
+  std::vector<Piece> pieces;
+  std::vector<int64_t> pbounds;  // world × (npieces + 1): piece boundaries of every rank
 };
 
 }  // namespace
@@ -113,6 +124,12 @@ struct qmfx_ctx {
   int64_t trace_cap = 0;
   // per-class timing: 0 direct kernel, 1 whitened kernels (row solve + unwhiten), 2 whole half
   hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};
+  // solve pieces per half (QMFX_PIECES; default 1 on one rank, 4 with several) and their
+  // events: [piece][start, direct done, whitened done]; collectives run on comm_stream
+  int npieces = 0;
+  hipEvent_t evp[QMFX_MAX_PIECES][3] = {};
+  hipEvent_t ev_sum = nullptr, ev_comm = nullptr;
+  hipStream_t comm_stream = nullptr;
   double cls_ms[3] = {0, 0, 0}, cls_flops[3] = {0, 0, 0}, cls_bytes[3] = {0, 0, 0};
   int64_t cls_launches[3] = {0, 0, 0};
 };
@@ -208,40 +225,75 @@ int max_whitened_ntn(const qmfx_ctx* c) {
 
 // Splits this rank's rows of `side` into whitened buckets (by padded signal count) and the
 // direct bucket (heaviest rows first, for load balance), and uploads the order list.
+int npieces(const qmfx_ctx* c) {
+  if (c->npieces > 0) return c->npieces;
+  return c->world > 1 ? 4 : 1;
+}
+
+// nnz-balanced split of rows [b, e) into p contiguous pieces → out[0..p]
+void split_rows(const std::vector<int64_t>& rp, int64_t b, int64_t e, int p, int64_t* out) {
+  out[0] = b;
+  out[p] = e;
+  for (int j = 1; j < p; ++j) {
+    const int64_t target = rp[b] + (int64_t)((__int128)(rp[e] - rp[b]) * j / p);
+    int64_t r = std::lower_bound(rp.begin() + b, rp.begin() + e + 1, target) - rp.begin();
+    out[j] = std::min(std::max(r, out[j - 1]), e);
+  }
+}
+
+// Splits this rank's rows of `side` into pieces, and each piece into whitened buckets (by
+// padded signal count) and the direct bucket (heaviest rows first, for load balance);
+// uploads the order list (piece sections back to back) and the per-slot descriptors.
 int build_buckets(qmfx_ctx* c, int side) {
   SideBuf& sb = c->s[side];
   sb.buckets_valid = false;
   if (sb.h_rowptr.empty()) return 0;
   if (sb.n > INT32_MAX) return fail("more than 2^31 rows on one side are not supported");
   const int mx = max_whitened_ntn(c);
-  std::vector<int64_t> wlist[4];
-  std::vector<std::pair<int64_t, int64_t>> direct;
+  const int P = npieces(c);
+  sb.pbounds.assign((size_t)c->world * (P + 1), 0);
+  for (int r = 0; r < c->world; ++r)
+    split_rows(sb.h_rowptr, sb.bounds[r], sb.bounds[r + 1], P, &sb.pbounds[(size_t)r * (P + 1)]);
   double nnz_w = 0, nnz_d = 0, flops_w = 0;
   const double k = c->k;
-  for (int64_t r = sb.rbeg; r < sb.rend; ++r) {
-    const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
-    const int64_t ntn = (std::max<int64_t>(n, 1) + 15) / 16;
-    if (ntn <= mx) {
-      wlist[ntn - 1].push_back(r);
-      nnz_w += (double)n;
-      // K (n(n+1)k), n×n Cholesky + solves (n³/3 + 2n²), Zᵀu and Zᵀc (4nk), unwhitening (2k²)
-      const double dn = (double)n;
-      flops_w += dn * (dn + 1) * k + dn * dn * dn / 3.0 + 2 * dn * dn + 4 * dn * k + 2 * k * k;
-    } else {
-      direct.emplace_back(n, r);
-      nnz_d += (double)n;
-    }
-  }
-  std::stable_sort(direct.begin(), direct.end(),
-                   [](const auto& x, const auto& y) { return x.first > y.first; });
   std::vector<int64_t> order;
   order.reserve(sb.rend - sb.rbeg);
-  for (int i = 0; i < 4; ++i) {
-    sb.wb[i] = (int64_t)order.size();
-    order.insert(order.end(), wlist[i].begin(), wlist[i].end());
+  sb.pieces.assign(P, SideBuf::Piece{});
+  int64_t nw_total = 0;
+  for (int j = 0; j < P; ++j) {
+    SideBuf::Piece& pc = sb.pieces[j];
+    pc.rb = sb.pbounds[(size_t)c->rank * (P + 1) + j];
+    pc.re = sb.pbounds[(size_t)c->rank * (P + 1) + j + 1];
+    pc.ord = (int64_t)order.size();
+    std::vector<int64_t> wlist[4];
+    std::vector<std::pair<int64_t, int64_t>> direct;
+    for (int64_t r = pc.rb; r < pc.re; ++r) {
+      const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
+      const int64_t ntn = (std::max<int64_t>(n, 1) + 15) / 16;
+      if (ntn <= mx) {
+        wlist[ntn - 1].push_back(r);
+        nnz_w += (double)n;
+        // K (n(n+1)k), n×n Cholesky + solves (n³/3 + 2n²), Zᵀu and Zᵀc (4nk), unwhitening (2k²)
+        const double dn = (double)n;
+        flops_w += dn * (dn + 1) * k + dn * dn * dn / 3.0 + 2 * dn * dn + 4 * dn * k + 2 * k * k;
+      } else {
+        direct.emplace_back(n, r);
+        nnz_d += (double)n;
+      }
+    }
+    std::stable_sort(direct.begin(), direct.end(),
+                     [](const auto& x, const auto& y) { return x.first > y.first; });
+    for (int i = 0; i < 4; ++i) {
+      pc.wb[i] = (int64_t)order.size() - pc.ord;
+      order.insert(order.end(), wlist[i].begin(), wlist[i].end());
+    }
+    pc.wb[4] = (int64_t)order.size() - pc.ord;
+    nw_total += pc.wb[4];
+    for (const auto& d : direct) order.push_back(d.second);
+    pc.n_ord = (int64_t)order.size() - pc.ord;
   }
-  sb.wb[4] = (int64_t)order.size();
-  for (const auto& d : direct) order.push_back(d.second);
+  for (int i = 0; i < 4; ++i) sb.wb[i] = 0;
+  sb.wb[4] = nw_total;  // whitened rows of this rank (all pieces)
   sb.n_ord = (int64_t)order.size();
   sb.nnz_w = nnz_w;
   sb.nnz_d = nnz_d;
@@ -291,6 +343,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->esz = precision == 32 ? 4 : 8;
   if (const char* ab = std::getenv("QMFX_ABLATE")) c->ablate = std::atoi(ab);
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
+  if (const char* np = std::getenv("QMFX_PIECES"))
+    c->npieces = std::min(std::max(std::atoi(np), 1), QMFX_MAX_PIECES);
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->G, (size_t)c->kp * c->kp * c->esz);
@@ -303,6 +357,10 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->evh[i]);
+  for (int i = 0; i < QMFX_MAX_PIECES && e == hipSuccess; ++i)
+    for (int j = 0; j < 3 && e == hipSuccess; ++j) e = hipEventCreate(&c->evp[i][j]);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_sum, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&c->Linv, (size_t)c->kp * c->kp * c->esz);
   if (e == hipSuccess) e = hipMalloc(&c->Gimg, (size_t)(nt * (nt + 1) / 2) * 256 * c->esz);
   if (e == hipSuccess) e = hipMalloc(&c->chol_status, sizeof(int32_t));
@@ -319,7 +377,14 @@ int qmfx_destroy(qmfx_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+  for (auto& row : c->evp)
+    for (auto& ev : row)
+      if (ev) (void)hipEventDestroy(ev);
+  if (c->ev_sum) (void)hipEventDestroy(c->ev_sum);
+  if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
   for (auto& sb : c->s) {
     dfree_t(sb.rowptr);
     dfree_t(sb.col);
@@ -627,7 +692,6 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   const int64_t rb = L.rbeg, re = L.rend, nrows = re - rb;
   const int64_t nW = L.wb[4];                   // whitened rows (buckets 0..3)
   const bool use_w = nW > 0 && lambda > 0.0;    // M = YᵀY + λI is SPD only for λ > 0
-  const int64_t d_begin = use_w ? L.wb[4] : 0;  // direct rows in the order list
   const bool fp32 = c->prec == 32;
   HIPCHK(hipEventRecord(c->evh[0], c->stream));
   // G = YᵀY of the fixed side (full replica on every rank)
@@ -672,7 +736,6 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
       HIPCHK(launch_gimg((const double*)c->G, c->nt, c->k, lambda, (double*)c->Gimg, c->stream));
   }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
-  // direct rows (heaviest first)
   const char* trace_path = std::getenv("QMFX_TRACE");
   if (trace_path && c->trace_cap < L.n_ord) {
     dfree_t(c->trace);
@@ -680,49 +743,75 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     c->trace_cap = L.n_ord;
   }
   if (trace_path) HIPCHK(hipMemsetAsync(c->trace, 0, (size_t)L.n_ord * 64, c->stream));
-  HIPCHK(hipEventRecord(c->ev0, c->stream));
-  const int64_t nD = L.n_ord - d_begin;
-  if (fp32) {
-    SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F, (const float*)c->G,
-                       (float*)L.F, c->rowloss, c->status, L.d_order, d_begin, nD,
-                       (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, (const float*)c->Gimg,
-                       trace_path ? c->trace : nullptr, (int32_t)R.n};
-    HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
-  } else {
-    SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
-                        (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
-                        d_begin, nD, alpha, lambda, c->k, c->ablate, L.d_desc,
-                        (const double*)c->Gimg, nullptr, (int32_t)R.n};
-    HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
-  }
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
-  if (use_w) {
-    for (int b = 0; b < 4; ++b) {
-      const int64_t cnt = L.wb[b + 1] - L.wb[b];
-      if (cnt <= 0) continue;
+  const bool dist = c->comm && c->world > 1;
+  const int P = (int)L.pieces.size();
+  int64_t nD = 0;
+  for (int j = 0; j < P; ++j) {
+    const SideBuf::Piece& pc = L.pieces[j];
+    // direct rows (heaviest first); all rows when the whitened form is off
+    const int64_t d0 = pc.ord + (use_w ? pc.wb[4] : 0);
+    const int64_t nd = pc.ord + pc.n_ord - d0;
+    nD += nd;
+    HIPCHK(hipEventRecord(c->evp[j][0], c->stream));
+    if (nd > 0) {
       if (fp32) {
-        SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
-                           (float*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
-                           (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
-                           trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
-        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+        SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F,
+                           (const float*)c->G, (float*)L.F, c->rowloss, c->status, L.d_order,
+                           d0, nd, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc,
+                           (const float*)c->Gimg, trace_path ? c->trace : nullptr,
+                           (int32_t)R.n};
+        HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
       } else {
-        SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z, nullptr,
-                            (double*)L.F, c->rowloss, c->status, L.d_order, L.wb[b], cnt,
-                            alpha, lambda, c->k, c->ablate, L.d_desc, nullptr, nullptr,
-                            (int32_t)c->z_cap};
-        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+        SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
+                            (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
+                            d0, nd, alpha, lambda, c->k, c->ablate, L.d_desc,
+                            (const double*)c->Gimg, nullptr, (int32_t)R.n};
+        HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
       }
     }
-    if (fp32)
-      HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order, nW, c->nt,
-                           (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
-    else
-      HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order, nW, c->nt,
-                           (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
+    HIPCHK(hipEventRecord(c->evp[j][1], c->stream));
+    // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
+    if (use_w && pc.wb[4] > 0) {
+      for (int b = 0; b < 4; ++b) {
+        const int64_t cnt = pc.wb[b + 1] - pc.wb[b];
+        if (cnt <= 0) continue;
+        if (fp32) {
+          SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
+                             (float*)L.F, c->rowloss, c->status, L.d_order, pc.ord + pc.wb[b],
+                             cnt, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
+                             trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
+          HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+        } else {
+          SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z,
+                              nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
+                              pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
+                              nullptr, nullptr, (int32_t)c->z_cap};
+          HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
+        }
+      }
+      if (fp32)
+        HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order + pc.ord, pc.wb[4], c->nt,
+                             (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
+      else
+        HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[4],
+                             c->nt, (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
+    }
+    HIPCHK(hipEventRecord(c->evp[j][2], c->stream));
+    if (dist) {
+      // piece j of every rank → every rank (an all-gather-v of contiguous row ranges), on
+      // the collective stream while the next piece is solved
+      HIPCHK(hipStreamWaitEvent(c->comm_stream, c->evp[j][2], 0));
+      NCCLCHK(ncclGroupStart());
+      for (int r = 0; r < c->world; ++r) {
+        const int64_t b = L.pbounds[(size_t)r * (P + 1) + j], e = L.pbounds[(size_t)r * (P + 1) + j + 1];
+        if (e <= b) continue;
+        char* base = (char*)L.F + (size_t)b * c->kp * c->esz;
+        NCCLCHK(ncclBroadcast(base, base, (size_t)(e - b) * c->kp, nccl_type(c->prec), r, c->comm,
+                              c->comm_stream));
+      }
+      NCCLCHK(ncclGroupEnd());
+    }
   }
-  HIPCHK(hipEventRecord(c->evh[1], c->stream));
   if (trace_path) {
     std::vector<uint64_t> h((size_t)L.n_ord * 8);
     HIPCHK(scopy(c, h.data(), c->trace, h.size() * 8, hipMemcpyDeviceToHost));
@@ -733,17 +822,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     }
   }
   HIPCHK(launch_sum_f64(c->rowloss + rb, nrows, c->dsum, c->stream));
-  if (c->comm && c->world > 1) {
-    NCCLCHK(ncclGroupStart());
-    for (int r = 0; r < c->world; ++r) {
-      const int64_t b = L.bounds[r], e = L.bounds[r + 1];
-      if (e <= b) continue;
-      char* base = (char*)L.F + (size_t)b * c->kp * c->esz;
-      NCCLCHK(ncclBroadcast(base, base, (size_t)(e - b) * c->kp, nccl_type(c->prec), r, c->comm,
-                            c->stream));
-    }
-    NCCLCHK(ncclGroupEnd());
-    NCCLCHK(ncclAllReduce(c->dsum, c->dsum, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+  if (dist) {
+    HIPCHK(hipEventRecord(c->ev_sum, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_sum, 0));
+    NCCLCHK(ncclAllReduce(c->dsum, c->dsum, 1, ncclFloat64, ncclSum, c->comm, c->comm_stream));
+    HIPCHK(hipEventRecord(c->ev_comm, c->comm_stream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
   }
   HIPCHK(hipEventRecord(c->evh[2], c->stream));
   HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -753,8 +837,13 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   if (chol_bad) return fail("YᵀY + λI is not positive definite", -5);
   // timing and algorithmic work per kernel class (SURVEY.md §8(d) accounting)
   float ms_d = 0.f, ms_w = 0.f, ms_h = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms_d, c->ev0, c->ev1));
-  HIPCHK(hipEventElapsedTime(&ms_w, c->ev1, c->evh[1]));
+  for (int j = 0; j < P; ++j) {
+    float t0 = 0.f, t1 = 0.f;
+    HIPCHK(hipEventElapsedTime(&t0, c->evp[j][0], c->evp[j][1]));
+    HIPCHK(hipEventElapsedTime(&t1, c->evp[j][1], c->evp[j][2]));
+    ms_d += t0;
+    ms_w += t1;
+  }
   HIPCHK(hipEventElapsedTime(&ms_h, c->evh[0], c->evh[2]));
   const double k = c->k, s = (double)c->esz;
   const double nzd = use_w ? L.nnz_d : L.nnz_d + L.nnz_w, nd = (double)nD;
@@ -788,6 +877,14 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   c->solve_bytes += by_d + by_w;
   c->last_side = side;
   if (loss_sum) *loss_sum = *c->hsum;
+  return 0;
+}
+
+int qmfx_wals_row_losses(qmfx_ctx* c, double* out) {
+  const SideBuf& L = c->s[c->last_side];
+  if (!c->rowloss || c->rowloss_cap < L.n) return fail("no half solved yet");
+  if (set_dev(c)) return -2;
+  HIPCHK(scopy(c, out, c->rowloss, (size_t)L.n * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1120,6 +1217,7 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
+    if (!c->comm_stream) HIPCHK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   }
   for (int side = 0; side < 2; ++side) {
     SideBuf& sb = c->s[side];

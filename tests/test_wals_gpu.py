@@ -208,3 +208,28 @@ def test_long_rows_fp32_direct(k):
         assert rel_err(c.factors(side), o.factors(side)) < 1e-4, side
         assert abs(ld - lo) < 1e-4 * abs(lo), side
         c.set_factors(side, o.factors(side))
+
+
+@pytest.mark.parametrize("k,precision,lam", [(64, 32, LAM), (128, 32, LAM), (32, 64, LAM),
+                                             (64, 32, 0.0)])
+def test_solve_pieces_bit_identical(k, precision, lam, monkeypatch):
+    """A half solved in several pieces (QMFX_PIECES: the multi-GPU schedule, where piece j
+    is all-gathered while piece j+1 is solved) must give bit-identical factors to the
+    one-piece solve (rows are independent).  The loss sum agrees to 1e-12 relative: a few
+    whitened rows' fp32 loss terms differ in the last bit with the launch layout.  Mixed row
+    lengths put whitened and direct rows in every piece; λ = 0 forces every row direct."""
+    u, i, v = synth(3000, 700, 60000, seed=5)
+    u = np.concatenate([u, np.full(300, 3001)])  # one heavy user
+    i = np.concatenate([i, np.arange(300)])
+    v = np.concatenate([v, np.ones(300)])
+    _, c1 = make_pair(u, i, v, k, precision, seed=4, lam=max(lam, LAM))
+    for pieces in (3, 7):
+        monkeypatch.setenv("QMFX_PIECES", str(pieces))
+        _, cp = make_pair(u, i, v, k, precision, seed=4, lam=max(lam, LAM))
+        monkeypatch.delenv("QMFX_PIECES")
+        c1.set_factors(1, cp.factors(1))
+        for side in (0, 1):
+            l1 = c1.wals_half(side, ALPHA, lam)
+            lp = cp.wals_half(side, ALPHA, lam)
+            assert np.array_equal(c1.factors(side), cp.factors(side)), (pieces, side)
+            assert abs(l1 - lp) <= 1e-12 * abs(l1), (pieces, side)
