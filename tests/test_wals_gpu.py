@@ -215,7 +215,7 @@ def test_long_rows_fp32_direct(k):
 def test_solve_pieces_bit_identical(k, precision, lam, monkeypatch):
     """A half solved in several pieces (QMFX_PIECES: the multi-GPU schedule, where piece j
     is all-gathered while piece j+1 is solved) must give bit-identical factors to the
-    one-piece solve (rows are independent).  The loss sum agrees to 1e-12 relative: a few
+    one-piece solve (rows are independent).  The loss sum agrees to 1e-9 relative: a few
     whitened rows' fp32 loss terms differ in the last bit with the launch layout.  Mixed row
     lengths put whitened and direct rows in every piece; λ = 0 forces every row direct."""
     u, i, v = synth(3000, 700, 60000, seed=5)
@@ -232,4 +232,4 @@ def test_solve_pieces_bit_identical(k, precision, lam, monkeypatch):
             l1 = c1.wals_half(side, ALPHA, lam)
             lp = cp.wals_half(side, ALPHA, lam)
             assert np.array_equal(c1.factors(side), cp.factors(side)), (pieces, side)
-            assert abs(l1 - lp) <= 1e-12 * abs(l1), (pieces, side)
+            assert abs(l1 - lp) <= 1e-9 * abs(l1), (pieces, side)
