@@ -13,6 +13,7 @@
 // order matches BPREngine::update exactly (p_u from the old q, q_i / q_n from the new p_u).
 #include "common.h"
 #include "kernels.h"
+#include "rowsolve.h"
 
 namespace qmfx {
 
@@ -110,23 +111,147 @@ __device__ __forceinline__ int64_t sample_negative(const int32_t* items, int64_t
   }
 }
 
+// Draws the negative for (slot, j) against the user's positives: the first 64 are staged in
+// `mine` (one per lane); longer lists are scanned from memory.
+template <typename A>
+__device__ __forceinline__ int64_t draw_negative_t(const A& a, const int32_t* items, int64_t cnt,
+                                                   int32_t mine, uint64_t key, int lane) {
+  if (cnt > 64) return sample_negative(items, cnt, a.nitems, key, lane);
+  for (uint32_t attempt = 0;; ++attempt) {
+    const uint64_t h = mix64(key ^ ((uint64_t)attempt << 48) ^ 0x5bd1e995ull);
+    const int64_t cand = (int64_t)(((unsigned __int128)h * (uint64_t)a.nitems) >> 64);
+    if (!__any(mine == (int32_t)cand) || attempt >= 4096) return cand;
+  }
+}
+
+// One positive's SGD steps (u, p, n_j), j = 0..num_neg-1, with the rows in registers: p_u
+// and q_p are loaded once and carried through the steps, as one thread of the reference
+// sees its own writes (BPREngine::update :178-220 per step); the negatives are drawn first
+// and their rows loaded together (a repeated negative takes the updated row of its earlier
+// draw).  Each row is stored after its last update.
+template <typename T, int E>
+__device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int64_t p,
+                                             const int64_t (&n)[4], int nn, int lane) {
+  const int kp = a.kp;
+  Row<T, E> pu, qp, qn[4];
+  load_row(pu, a.U + u * kp, lane, kp);
+  load_row(qp, a.I + p * kp, lane, kp);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < nn) load_row(qn[j], a.I + n[j] * kp, lane, kp);
+  T bp = T(0), bn[4] = {T(0), T(0), T(0), T(0)};
+  if (a.use_biases) {
+    bp = ld_shared(a.bias + p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < nn) bn[j] = ld_shared(a.bias + n[j]);
+  }
+  bool ok = true;
+  const T lr = a.lr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nn) break;
+    // a negative drawn twice continues from its updated row
+#pragma unroll
+    for (int i = 0; i < j; ++i)
+      if (n[i] == n[j]) {
+        qn[j] = qn[i];
+        bn[j] = bn[i];
+      }
+    T part = T(0);
+#pragma unroll
+    for (int e = 0; e < E; ++e) part += pu.v[e] * (qp.v[e] - qn[j].v[e]);
+    T x = wave_sum(part);
+    if (a.use_biases) x += bp - bn[j];
+    const T eg = T(1) / (T(1) + exp(x));
+    if (!isfinite(eg)) {
+      ok = false;
+      continue;  // the reference aborts (CHECK); the row is left as it was
+    }
+    if (a.use_biases) {
+      bp = bp + lr * (eg - a.bias_lambda * bp);
+      bn[j] = bn[j] + lr * (-eg - a.bias_lambda * bn[j]);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const T pu_new = pu.v[e] + lr * (eg * (qp.v[e] - qn[j].v[e]) - a.user_lambda * pu.v[e]);
+      const T qp_new = qp.v[e] + lr * (eg * pu_new - a.item_lambda * qp.v[e]);
+      const T qn_new = qn[j].v[e] + lr * (-eg * pu_new - a.item_lambda * qn[j].v[e]);
+      pu.v[e] = pu_new;
+      qp.v[e] = qp_new;
+      qn[j].v[e] = qn_new;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nn) break;
+    bool last = true;
+#pragma unroll
+    for (int i = j + 1; i < 4; ++i)
+      if (i < nn && n[i] == n[j]) last = false;
+    if (last) {
+      store_row(qn[j], a.I + n[j] * kp, lane, kp);
+      if (a.use_biases && lane == 0) st_shared(a.bias + n[j], bn[j]);
+    }
+  }
+  store_row(pu, a.U + u * kp, lane, kp);
+  store_row(qp, a.I + p * kp, lane, kp);
+  if (a.use_biases && lane == 0) st_shared(a.bias + p, bp);
+  return ok;
+}
+
+// Hogwild epoch: each wave walks positives i = wave, wave + nwaves, ... in the epoch's
+// permuted order.  Positive i's data arrives through a 3-stage prefetch, one stage per
+// iteration: (user, item) three positives ahead, the user's CSR range two ahead, its staged
+// positive list one ahead.  They are issued before the current positive's row loads, so
+// each iteration waits for about one memory latency instead of a chain of dependent loads.
 template <typename T, int E>
 __global__ __launch_bounds__(64) void bpr_epoch_kernel(BprArgs<T> a) {
   const int lane = threadIdx.x;
-  const int64_t nwaves = (int64_t)gridDim.x;
+  const int64_t nw = (int64_t)gridDim.x;
+  // slot of positive i = (perm_a·i + perm_b) mod npos: one 128-bit reduction per wave, then
+  // a running sum (step = perm_a·nw mod npos; positives past the end get valid, unused slots)
+  const uint64_t np = (uint64_t)a.npos;
+  const uint64_t step = (uint64_t)(((unsigned __int128)a.perm_a * (uint64_t)gridDim.x) % np);
+  auto advance = [&](uint64_t sl) {
+    sl += step;
+    return sl >= np ? sl - np : sl;
+  };
+  int64_t i = blockIdx.x;
+  if (i >= a.npos) return;
   bool ok = true;
-  for (int64_t i = blockIdx.x; i < a.npos; i += nwaves) {
-    const int64_t slot = (int64_t)(((unsigned __int128)a.perm_a * (uint64_t)i + a.perm_b) %
-                                   (uint64_t)a.npos);
-    const int64_t u = a.pos_user[slot];
-    const int64_t p = a.pos_item[slot];
-    const int64_t rb = a.urowptr[u];
-    const int64_t cnt = a.urowptr[u + 1] - rb;
-    for (int j = 0; j < a.num_neg; ++j) {
-      const uint64_t key = mix64(a.seed ^ mix64((uint64_t)slot * 64ull + (uint64_t)j));
-      const int64_t n = sample_negative(a.uitems + rb, cnt, a.nitems, key, lane);
-      ok &= bpr_step<T, E>(a, u, p, n, lane);
+  // stage 0 (current): everything; stage 1: + CSR range; stage 2: (user, item)
+  uint64_t s0 = (uint64_t)(((unsigned __int128)a.perm_a * (uint64_t)i + a.perm_b) % np);
+  uint64_t s1 = advance(s0), s2 = advance(s1), s3 = s2;
+  int64_t slot0 = (int64_t)s0, u0 = a.pos_user[slot0], p0 = a.pos_item[slot0];
+  int64_t rb0 = a.urowptr[u0], cnt0 = a.urowptr[u0 + 1] - rb0;
+  // (every lane loads: an unconditional load keeps the wait counts exact)
+  int32_t mine0 = a.uitems[rb0 + (lane < cnt0 ? lane : 0)];
+  mine0 = lane < cnt0 ? mine0 : -1;
+  int64_t slot1 = (int64_t)s1, u1 = a.pos_user[slot1], p1 = a.pos_item[slot1];
+  int64_t rb1 = a.urowptr[u1], cnt1 = a.urowptr[u1 + 1] - rb1;
+  int64_t slot2 = (int64_t)s2, u2 = a.pos_user[slot2], p2 = a.pos_item[slot2];
+  for (; i < a.npos; i += nw) {
+    s3 = advance(s3);
+    const int64_t slot3 = (int64_t)s3;
+    const int64_t u3 = a.pos_user[slot3], p3 = a.pos_item[slot3];
+    const int64_t rb2 = a.urowptr[u2], cnt2 = a.urowptr[u2 + 1] - rb2;
+    int32_t mine1 = a.uitems[rb1 + (lane < cnt1 ? lane : 0)];
+    for (int j0 = 0; j0 < a.num_neg; j0 += 4) {
+      const int nn = a.num_neg - j0 < 4 ? a.num_neg - j0 : 4;
+      int64_t n[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < nn) {
+          const uint64_t key = mix64(a.seed ^ mix64((uint64_t)slot0 * 64ull + (uint64_t)(j0 + j)));
+          n[j] = draw_negative_t(a, a.uitems + rb0, cnt0, mine0, key, lane);
+        }
+      ok &= bpr_positive<T, E>(a, u0, p0, n, nn, lane);
     }
+    mine1 = lane < cnt1 ? mine1 : -1;
+    slot0 = slot1, u0 = u1, p0 = p1, rb0 = rb1, cnt0 = cnt1, mine0 = mine1;
+    slot1 = slot2, u1 = u2, p1 = p2, rb1 = rb2, cnt1 = cnt2;
+    slot2 = slot3, u2 = u3, p2 = p3;
   }
   if (!ok && lane == 0) *a.bad = 1;
 }
@@ -142,29 +267,33 @@ __global__ __launch_bounds__(64) void bpr_apply_kernel(BprArgs<T> a, const int64
   if (!ok && lane == 0) *a.bad = 1;
 }
 
-// Σ log(1 + exp(−x̂)) over eval triplets (BPREngine::evaluate :246-274): one wave per
-// triplet, per-block partials, then a fixed-order sum.
-template <typename T, int E>
+// Σ log(1 + exp(−x̂)) over eval triplets (BPREngine::evaluate :246-274).  Each wave scores
+// four triplets at a time, 16 lanes per triplet and NT = KP/16 contiguous factors per lane
+// (one 16-B load per row and lane at k = 64), so 4× as many rows are in flight as with a
+// wave per triplet; per-block partials, then a fixed-order sum.
+template <typename T, int NT>
 __global__ __launch_bounds__(256) void bpr_eval_kernel(const T* U, const T* I, const T* bias,
                                                        const int64_t* trip, int64_t n, int kp,
                                                        int use_biases, double* partial) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int g = lane >> 4, c = lane & 15;
+  const int64_t stride = (int64_t)gridDim.x * 16;
   double s = 0.0;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < n; t += nw) {
+  for (int64_t t = ((int64_t)blockIdx.x * 4 + w) * 4 + g; t < n; t += stride) {
     const int64_t u = trip[3 * t], p = trip[3 * t + 1], q = trip[3 * t + 2];
+    const T* pu = U + u * kp + c * NT;
+    const T* qp = I + p * kp + c * NT;
+    const T* qn = I + q * kp + c * NT;
     T part = T(0);
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int f = lane + 64 * e;
-      if (f < kp) part += U[u * kp + f] * (I[p * kp + f] - I[q * kp + f]);
-    }
-    T x = wave_sum(part);
+    for (int e = 0; e < NT; ++e) part += pu[e] * (qp[e] - qn[e]);
+    T x = row16_sum(part);
     if (use_biases) x += bias[p] - bias[q];
-    s += log(1.0 + exp(-(double)x));
+    if (c == 0) s += log(1.0 + exp(-(double)x));
   }
+  s = wave_sum(s);
   if (lane == 0) red[w] = s;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
@@ -188,6 +317,17 @@ __global__ void sum_partials_kernel(const double* partial, int n, double* out) {
     default: return hipErrorInvalidValue; \
   }
 
+#define QMFX_NT_SWITCH(KP, CALL)                                            \
+  switch ((KP) / 16) {                                                      \
+    case 1: return CALL(1);   case 2: return CALL(2);   case 3: return CALL(3);   \
+    case 4: return CALL(4);   case 5: return CALL(5);   case 6: return CALL(6);   \
+    case 7: return CALL(7);   case 8: return CALL(8);   case 9: return CALL(9);   \
+    case 10: return CALL(10); case 11: return CALL(11); case 12: return CALL(12); \
+    case 13: return CALL(13); case 14: return CALL(14); case 15: return CALL(15); \
+    case 16: return CALL(16);                                               \
+    default: return hipErrorInvalidValue;                                   \
+  }
+
 template <typename T, int E>
 static hipError_t bpr_epoch(const BprArgs<T>& a, hipStream_t s) {
   hipLaunchKernelGGL((bpr_epoch_kernel<T, E>), dim3(a.waves), dim3(64), 0, s, a);
@@ -199,12 +339,12 @@ static hipError_t bpr_apply(const BprArgs<T>& a, const int64_t* trip, int64_t n,
   hipLaunchKernelGGL((bpr_apply_kernel<T, E>), dim3(1), dim3(64), 0, s, a, trip, n);
   return hipGetLastError();
 }
-template <typename T, int E>
+template <typename T, int NT>
 static hipError_t bpr_eval(const T* U, const T* I, const T* bias, const int64_t* trip,
                            int64_t n, int kp, int use_biases, double* partial, double* out,
                            hipStream_t s) {
-  const int grid = 1024;
-  hipLaunchKernelGGL((bpr_eval_kernel<T, E>), dim3(grid), dim3(256), 0, s, U, I, bias, trip, n,
+  const int grid = 1024;  // = the context's partial buffer
+  hipLaunchKernelGGL((bpr_eval_kernel<T, NT>), dim3(grid), dim3(256), 0, s, U, I, bias, trip, n,
                      kp, use_biases, partial);
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, s, partial, grid, out);
   return hipGetLastError();
@@ -235,15 +375,15 @@ hipError_t launch_bpr_apply_f64(const BprArgs<double>& a, const int64_t* trip, i
 hipError_t launch_bpr_eval_f32(const float* U, const float* I, const float* bias,
                                const int64_t* trip, int64_t n, int kp, int use_biases,
                                double* partial, double* out, hipStream_t s) {
-#define CALL(E) bpr_eval<float, E>(U, I, bias, trip, n, kp, use_biases, partial, out, s)
-  QMFX_E_SWITCH(kp, CALL)
+#define CALL(NT) bpr_eval<float, NT>(U, I, bias, trip, n, kp, use_biases, partial, out, s)
+  QMFX_NT_SWITCH(kp, CALL)
 #undef CALL
 }
 hipError_t launch_bpr_eval_f64(const double* U, const double* I, const double* bias,
                                const int64_t* trip, int64_t n, int kp, int use_biases,
                                double* partial, double* out, hipStream_t s) {
-#define CALL(E) bpr_eval<double, E>(U, I, bias, trip, n, kp, use_biases, partial, out, s)
-  QMFX_E_SWITCH(kp, CALL)
+#define CALL(NT) bpr_eval<double, NT>(U, I, bias, trip, n, kp, use_biases, partial, out, s)
+  QMFX_NT_SWITCH(kp, CALL)
 #undef CALL
 }
 

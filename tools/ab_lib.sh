@@ -5,7 +5,5 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 for lib in "$@"; do
   QMFX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --config ${CFG:-c3} --no-cpu-baseline --steps ${STEPS:-2} > gpurun_out/ab.json 2> gpurun_out/ab.err || { echo "bench failed: $lib"; tail -5 gpurun_out/ab.err; exit 1; }
-  python3 -c "
-import json; d=json.load(open('gpurun_out/ab.json')); r=d['roofline']
-print('$lib |', d['ms_per_step'], 'ms/epoch |', {k:round(v['launch_ms'],2) for k,v in r['classes'].items()})"
+  python3 tools/ab_print.py gpurun_out/ab.json "$lib"
 done
