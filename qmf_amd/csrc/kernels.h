@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace qmfx {
 
@@ -38,6 +39,26 @@ struct SolveArgs {
   int32_t zrow;           // whitened kernel: index of an all-zero row of Y (padding signals)
 };
 
+// Per-row kernels take one workgroup per row (slot = row_begin + blockIdx.x).  A launch's
+// total thread count must fit 32 bits (10M rows × 512 threads does not), so rows go out in
+// chunks of at most 2^31 / threads workgroups.
+// (QMFX_ROW_CHUNK lowers the chunk for the tests.)
+template <typename T, typename F>
+hipError_t launch_row_chunks(const SolveArgs<T>& a, int threads, F launch) {
+  int64_t cap = ((int64_t)1 << 31) / threads;
+  if (const char* e = std::getenv("QMFX_ROW_CHUNK"))
+    if (std::atoll(e) > 0 && std::atoll(e) < cap) cap = std::atoll(e);
+  for (int64_t done = 0; done < a.nrows; done += cap) {
+    SolveArgs<T> c = a;
+    c.row_begin = a.row_begin + done;
+    c.nrows = a.nrows - done < cap ? a.nrows - done : cap;
+    launch(c);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 // G + λI (padding diagonal 1) → the direct row kernel's accumulator-tile image
 hipError_t launch_gimg(const float* G, int nt, int k, double lambda, float* img, hipStream_t s);
 hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* img, hipStream_t s);
@@ -59,10 +80,11 @@ hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int6
 hipError_t launch_whiten(const double* in, double* out, const int64_t* order, int64_t nrows,
                          int nt, const double* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s);
+// scratch: KP·(KP+1) doubles, used when KP > 128 (the fp64 matrix does not fit LDS)
 hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
-                           int32_t* status, hipStream_t s);
+                           int32_t* status, double* scratch, hipStream_t s);
 hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
-                           int32_t* status, hipStream_t s);
+                           int32_t* status, double* scratch, hipStream_t s);
 hipError_t launch_gram(const float* Y, int64_t n, int nt, float* G, double* partial,
                        int max_blocks, hipStream_t s);
 hipError_t launch_gram(const double* Y, int64_t n, int nt, double* G, double* partial,

@@ -119,6 +119,7 @@ struct qmfx_ctx {
   int64_t z_cap = 0;
   void* Linv = nullptr;  // kp × kp
   int32_t* chol_status = nullptr;
+  double* chol_scratch = nullptr;  // KP > 128: the fp64 factorization of G + λI (global)
   void* Gimg = nullptr;  // G + λI as the direct kernel's accumulator-tile image
   uint64_t* trace = nullptr;  // QMFX_TRACE diagnostics: whitened-row phase timestamps
   int64_t trace_cap = 0;
@@ -216,7 +217,9 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
 
 int max_whitened_ntn(const qmfx_ctx* c) {
-  if (!c->whitened_enabled || use_big(c)) return 0;
+  if (!c->whitened_enabled) return 0;
+  // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) only
+  if (use_big(c)) return c->prec == 32 && c->nt == 16 ? 4 : 0;
   int m = c->nt / 2;
   if (m > 4) m = 4;
   if (c->prec == 64 && m > 2) m = 2;
@@ -364,6 +367,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipMalloc(&c->Linv, (size_t)c->kp * c->kp * c->esz);
   if (e == hipSuccess) e = hipMalloc(&c->Gimg, (size_t)(nt * (nt + 1) / 2) * 256 * c->esz);
   if (e == hipSuccess) e = hipMalloc(&c->chol_status, sizeof(int32_t));
+  if (e == hipSuccess && c->kp > 128)
+    e = hipMalloc(&c->chol_scratch, (size_t)c->kp * (c->kp + 1) * sizeof(double));
   if (e != hipSuccess) {
     g_err = std::string("qmfx_create: ") + hipGetErrorString(e);
     delete c;
@@ -417,6 +422,7 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree(c->Gimg);
   dfree_t(c->trace);
   dfree_t(c->chol_status);
+  dfree_t(c->chol_scratch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -719,12 +725,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     HIPCHK(hipMemsetAsync(c->chol_status, 0, 4, c->stream));
     if (fp32) {
       HIPCHK(launch_chol_inv((const float*)c->G, c->nt, c->k, lambda, (float*)c->Linv,
-                             c->chol_status, c->stream));
+                             c->chol_status, c->chol_scratch, c->stream));
       HIPCHK(launch_whiten((const float*)R.F, (float*)c->Z, nullptr, R.n, c->nt,
                            (const float*)c->Linv, nullptr, 0.0, false, c->stream));
     } else {
       HIPCHK(launch_chol_inv((const double*)c->G, c->nt, c->k, lambda, (double*)c->Linv,
-                             c->chol_status, c->stream));
+                             c->chol_status, c->chol_scratch, c->stream));
       HIPCHK(launch_whiten((const double*)R.F, (double*)c->Z, nullptr, R.n, c->nt,
                            (const double*)c->Linv, nullptr, 0.0, false, c->stream));
     }

@@ -633,7 +633,7 @@ __global__ void gimg_kernel(const T* G, int k, double lambda, T* img) {
 // Writes x' (whitened); whiten_kernel<UNWHITEN> maps it to x = L⁻ᵀ x' and adds −λ‖x‖².
 // ---------------------------------------------------------------------------------------
 template <typename T, int NTK, int NTN, bool TRACE>
-__global__ __launch_bounds__(64, 2) void wals_woodbury_kernel(SolveArgs<T> a) {
+__global__ __launch_bounds__(64, NTK > 8 ? 1 : 2) void wals_woodbury_kernel(SolveArgs<T> a) {
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   using v4 = typename M::acc_t;  // 4-wide vector of T
@@ -1108,11 +1108,12 @@ template <typename T, int NT>
 static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc || !a.Gimg) return hipErrorInvalidValue;
-  if (a.trace)
-    hipLaunchKernelGGL((wals_direct_kernel<T, NT, true>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
-  else
-    hipLaunchKernelGGL((wals_direct_kernel<T, NT, false>), dim3((unsigned)a.nrows), dim3(64), 0, s, a);
-  return hipGetLastError();
+  return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {
+    if (c.trace)
+      hipLaunchKernelGGL((wals_direct_kernel<T, NT, true>), dim3((unsigned)c.nrows), dim3(64), 0, s, c);
+    else
+      hipLaunchKernelGGL((wals_direct_kernel<T, NT, false>), dim3((unsigned)c.nrows), dim3(64), 0, s, c);
+  });
 }
 
 template <typename T, int NT>
@@ -1128,10 +1129,12 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
 #define QMFX_WB(N)                                                                            \
-  if (a.trace)                                                                                \
-    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, true>), dim3((unsigned)a.nrows), b, 0, s, a); \
-  else                                                                                        \
-    hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, false>), dim3((unsigned)a.nrows), b, 0, s, a)
+  return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                                \
+    if (c.trace)                                                                              \
+      hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, true>), dim3((unsigned)c.nrows), b, 0, s, c); \
+    else                                                                                      \
+      hipLaunchKernelGGL((wals_woodbury_kernel<T, NTK, N, false>), dim3((unsigned)c.nrows), b, 0, s, c); \
+  })
   if (ntn == 1) {
     QMFX_WB(1);
   } else if (ntn == 2) {
@@ -1165,11 +1168,74 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
   return hipGetLastError();
 }
 
+// The same factorization for KP > 128 (the fp64 matrix exceeds LDS): one 1024-thread
+// workgroup on a global fp64 scratch of KP·(KP+1) doubles (L2-resident; __syncthreads
+// orders the block's global accesses).  Once per half; ≈ms at KP = 256.
+template <typename T, int NT>
+__global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k, double lambda,
+                                                               T* Linv, int32_t* status,
+                                                               double* A) {
+  constexpr int KP = 16 * NT;
+  constexpr int LD = KP + 1;
+  __shared__ double dinv[KP];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < KP * KP; idx += 1024) {
+    const int i = idx / KP, j = idx % KP;
+    double v = (double)G[idx];
+    if (i == j) v += i < k ? lambda : 1.0;
+    A[i * LD + j] = v;
+  }
+  __syncthreads();
+  for (int j = 0; j < KP; ++j) {
+    if (tid == 0) {
+      const double d = A[j * LD + j];
+      if (!(d > 0.0)) *status = 1;
+      const double l = sqrt(d > 0.0 ? d : 1.0);
+      A[j * LD + j] = l;
+      dinv[j] = 1.0 / l;
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < KP; i += 1024) A[i * LD + j] *= dinv[j];
+    __syncthreads();
+    const int m = KP - j - 1;
+    for (int idx = tid; idx < m * m; idx += 1024) {
+      const int ii = j + 1 + idx / m, mm = j + 1 + idx % m;
+      if (mm <= ii) A[ii * LD + mm] -= A[ii * LD + j] * A[mm * LD + j];
+    }
+    __syncthreads();
+  }
+  if (tid < KP) {
+    const int c = tid;
+    for (int i = c + 1; i < KP; ++i) {
+      double sm = A[i * LD + c] * dinv[c];
+      for (int mm = c + 1; mm < i; ++mm) sm += A[i * LD + mm] * A[c * LD + mm];
+      A[c * LD + i] = -sm * dinv[i];
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < KP * KP; idx += 1024) {
+    const int i = idx / KP, c = idx % KP;
+    double v = 0.0;
+    if (i == c) v = dinv[c];
+    else if (i > c) v = A[c * LD + i];
+    Linv[idx] = (T)v;
+  }
+}
+
 template <typename T, int NT>
 static hipError_t launch_chol_inv_nt(const T* G, int k, double lambda, T* Linv, int32_t* status,
-                                     hipStream_t s) {
-  hipLaunchKernelGGL((chol_inv_kernel<T, NT>), dim3(1), dim3(256), 0, s, G, k, lambda, Linv, status);
-  return hipGetLastError();
+                                     double* scratch, hipStream_t s) {
+  if constexpr (NT > 8) {
+    if (!scratch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((chol_inv_global_kernel<T, NT>), dim3(1), dim3(1024), 0, s, G, k, lambda,
+                       Linv, status, scratch);
+    return hipGetLastError();
+  } else {
+    (void)scratch;
+    hipLaunchKernelGGL((chol_inv_kernel<T, NT>), dim3(1), dim3(256), 0, s, G, k, lambda, Linv,
+                       status);
+    return hipGetLastError();
+  }
 }
 
 template <typename T, int NT>
@@ -1199,6 +1265,21 @@ static hipError_t launch_gram_nt(const T* Y, int64_t n, T* G, double* partial,
     case 6: return CALL(6);               \
     case 7: return CALL(7);               \
     case 8: return CALL(8);               \
+    default: return hipErrorInvalidValue; \
+  }
+// fp32 whitened path: every one-wave tiling plus k = 256 (NT = 16, beside the multi-wave
+// direct kernel)
+#define QMFX_NT_SWITCH_W(NTV, CALL)       \
+  switch (NTV) {                          \
+    case 1: return CALL(1);               \
+    case 2: return CALL(2);               \
+    case 3: return CALL(3);               \
+    case 4: return CALL(4);               \
+    case 5: return CALL(5);               \
+    case 6: return CALL(6);               \
+    case 7: return CALL(7);               \
+    case 8: return CALL(8);               \
+    case 16: return CALL(16);             \
     default: return hipErrorInvalidValue; \
   }
 #define QMFX_NT_SWITCH64(NTV, CALL)       \
@@ -1233,7 +1314,7 @@ hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s)
 }
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {
 #define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, s)
-  QMFX_NT_SWITCH(nt, CALL)
+  QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
@@ -1245,7 +1326,7 @@ hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int6
                          int nt, const float* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s) {
 #define CALL(N) launch_whiten_nt<float, N>(in, out, order, nrows, Linv, rowloss, lambda, unwhiten, s)
-  QMFX_NT_SWITCH(nt, CALL)
+  QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 hipError_t launch_whiten(const double* in, double* out, const int64_t* order, int64_t nrows,
@@ -1256,14 +1337,14 @@ hipError_t launch_whiten(const double* in, double* out, const int64_t* order, in
 #undef CALL
 }
 hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
-                           int32_t* status, hipStream_t s) {
-#define CALL(N) launch_chol_inv_nt<float, N>(G, k, lambda, Linv, status, s)
-  QMFX_NT_SWITCH(nt, CALL)
+                           int32_t* status, double* scratch, hipStream_t s) {
+#define CALL(N) launch_chol_inv_nt<float, N>(G, k, lambda, Linv, status, scratch, s)
+  QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
-                           int32_t* status, hipStream_t s) {
-#define CALL(N) launch_chol_inv_nt<double, N>(G, k, lambda, Linv, status, s)
+                           int32_t* status, double* scratch, hipStream_t s) {
+#define CALL(N) launch_chol_inv_nt<double, N>(G, k, lambda, Linv, status, scratch, s)
   QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
 }

@@ -398,9 +398,10 @@ __global__ void gram_reduce_rt_kernel(const double* partial, int nblocks, int nt
 template <typename T, int NT>
 static hipError_t launch_big_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
-  hipLaunchKernelGGL((wals_big_kernel<T, NT>), dim3((unsigned)a.nrows), dim3(BigCfg<T, NT>::NTHR),
-                     0, s, a);
-  return hipGetLastError();
+  return launch_row_chunks(a, BigCfg<T, NT>::NTHR, [&](const SolveArgs<T>& c) {
+    hipLaunchKernelGGL((wals_big_kernel<T, NT>), dim3((unsigned)c.nrows),
+                       dim3(BigCfg<T, NT>::NTHR), 0, s, c);
+  });
 }
 
 template <typename T, int NT>

@@ -147,7 +147,7 @@ def test_indefinite_rows_are_flagged():
     assert 0 in set(c.failed_rows().tolist())
 
 
-@pytest.mark.parametrize("k,precision", [(128, 32), (64, 32), (64, 64), (32, 64)])
+@pytest.mark.parametrize("k,precision", [(256, 32), (128, 32), (64, 32), (64, 64), (32, 64)])
 def test_whitened_rows_match_direct_and_oracle(k, precision, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
@@ -233,3 +233,19 @@ def test_solve_pieces_bit_identical(k, precision, lam, monkeypatch):
             lp = cp.wals_half(side, ALPHA, lam)
             assert np.array_equal(c1.factors(side), cp.factors(side)), (pieces, side)
             assert abs(l1 - lp) <= 1e-9 * abs(l1), (pieces, side)
+
+
+@pytest.mark.parametrize("k", [256, 128])
+def test_row_chunked_launches_bit_identical(k, monkeypatch):
+    """Per-row kernels are launched in chunks below 2^31 threads (10M rows × 512 threads of
+    the k = 256 kernel overflowed a single launch and silently skipped rows).  Forcing tiny
+    chunks (QMFX_ROW_CHUNK) must not change a single bit."""
+    u, i, v = synth(1200, 300, 30000, seed=9)
+    _, c1 = make_pair(u, i, v, k, 32, seed=6)
+    monkeypatch.setenv("QMFX_ROW_CHUNK", "37")
+    _, c2 = make_pair(u, i, v, k, 32, seed=6)
+    for side in (0, 1):
+        l1 = c1.wals_half(side, ALPHA, LAM)
+        l2 = c2.wals_half(side, ALPHA, LAM)
+        assert np.array_equal(c1.factors(side), c2.factors(side)), side
+        assert l1 == l2, side
