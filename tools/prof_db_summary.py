@@ -21,7 +21,8 @@ def main(path, out=sys.stdout):
         c = sqlite3.connect(db)
         for name, calls, tot, avg, pct in c.execute(
                 "select name, total_calls, total_duration, average, percentage from top_kernels"):
-            w.writerow([short(name), calls, round(tot), round(avg), round(pct, 3)])
+            # the rocpd top_kernels view reports microseconds
+            w.writerow([short(name), calls, round(tot * 1e3), round(avg * 1e3), round(pct, 3)])
 
 
 if __name__ == "__main__":
