@@ -117,6 +117,23 @@ int qmfx_bpr_apply(qmfx_ctx* ctx, const int64_t* triplets, int64_t n, double lr,
 int qmfx_bpr_eval(qmfx_ctx* ctx, int slot, const int64_t* triplets, int64_t n, int use_biases,
                   double* loss_sum);
 
+/* ---- test-set evaluation (Engine::computeTestScores Engine.cpp:73-96 + Metrics.cpp:27-164)
+ * The device replaces the dense n_test × n_items score matrix by the statistics every
+ * reference metric (mse, auc, ap, p@k, r@k) is a function of.
+ * qmfx_eval_set_labels: test users (user idx, ntest of them) and their labelled items as a
+ * CSR over the test slots (rowptr[ntest+1], item idx, label value; zero labels may be left
+ * out).  Labels > 0 are the positives.  Cached on the context until the next call. */
+int qmfx_eval_set_labels(qmfx_ctx* ctx, int64_t ntest, const int64_t* users,
+                         const int64_t* rowptr, const int64_t* items, const double* values);
+/* Scores the current factors (score = [bias_i +] <u, q_i>, the reference's double, bit for
+ * bit; use_biases adds the context's item biases) and returns
+ *   label_scores[rowptr[ntest]]  the score of every labelled pair, in CSR order;
+ *   above[npos]                  per positive (labelled pair with value > 0, in CSR order):
+ *                                the number of items scored strictly higher;
+ *   sq_sum[ntest]                Σ over all items of score². */
+int qmfx_eval_ranks(qmfx_ctx* ctx, int use_biases, double* label_scores, int64_t* above,
+                    double* sq_sum);
+
 /* ---- multi-GPU (one process per GPU; RCCL over xGMI) -------------------------------------- */
 int qmfx_rccl_unique_id(uint8_t* id128);
 int qmfx_dist_init(qmfx_ctx* ctx, int rank, int world, const uint8_t* id128);

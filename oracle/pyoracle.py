@@ -260,3 +260,79 @@ def bpr_sets(users, items, values, test=None, eval_num_neg=3, eval_seed=42):
     if rc:
         raise ValueError("a user has every item as a positive")
     return uids[:nu.value], iids[:ni.value], ev[:ne.value], tev[:nt.value]
+
+
+# ---- test-set evaluation (numpy restatement; test infrastructure) ---------------------------
+def test_scores(U, I, users, bias=None):
+    """Engine::computeTestScores (Engine.cpp:73-96): score = bias_i (or 0), then += u_f·q_f in
+    factor order.  numpy's elementwise multiply and add round each step like the reference's
+    double loop (no fused multiply-add), so the scores are the reference's bit for bit."""
+    U = np.asarray(U, np.float64)
+    I = np.asarray(I, np.float64)
+    out = np.empty((len(users), I.shape[0]))
+    for t, u in enumerate(users):
+        s = np.zeros(I.shape[0]) if bias is None else np.array(bias, np.float64)
+        for f in range(I.shape[1]):
+            s = s + U[u, f] * I[:, f]
+        out[t] = s
+    return out
+
+
+def _sorted_pairs(labels, scores):
+    # (score, label > 0) pairs sorted descending as std::greater<pair<Double, bool>>
+    pos = np.asarray(labels) > 0.0
+    order = np.lexsort((pos, np.asarray(scores)))[::-1]
+    return pos[order]
+
+
+def metric_mse(labels, scores):
+    """MeanSquaredError::compute, Metrics.cpp:59-69 (sequential sum: cumsum)."""
+    d = np.asarray(labels, np.float64) - np.asarray(scores, np.float64)
+    assert len(d) > 0
+    return np.cumsum(d * d)[-1] / len(d)
+
+
+def metric_auc(labels, scores):
+    """AUC::compute, Metrics.cpp:71-106: each negative adds tp/pos/neg in sorted order."""
+    p = _sorted_pairs(labels, scores)
+    pos = int(p.sum())
+    neg = len(p) - pos
+    if pos == 0 or neg == 0:
+        return 1.0
+    tp = np.cumsum(p)
+    terms = tp[~p].astype(np.float64) / pos / neg
+    return float(np.cumsum(terms)[-1]) if len(terms) else 0.0
+
+
+def metric_precision(labels, scores, k):
+    """Precision::compute, Metrics.cpp:108-122 (positives among the k best pairs)."""
+    assert len(labels) >= k
+    return float(_sorted_pairs(labels, scores)[:k].sum()) / k
+
+
+def metric_recall(labels, scores, k):
+    """Recall::compute, Metrics.cpp:124-145."""
+    assert len(labels) >= k
+    p = _sorted_pairs(labels, scores)
+    assert p.sum() > 0
+    return float(p[:k].sum()) / int(p.sum())
+
+
+def metric_ap(labels, scores):
+    """AveragePrecision::compute, Metrics.cpp:147-163."""
+    p = _sorted_pairs(labels, scores)
+    tot = int(p.sum())
+    assert tot > 0
+    r = np.nonzero(p)[0]
+    terms = np.arange(1, tot + 1, dtype=np.float64) / (r + 1)
+    return float(np.cumsum(terms)[-1]) / tot
+
+
+def rank_stats(labels, scores):
+    """What qmfx_eval_ranks returns for one user, by brute force: Σ score², and per positive
+    (label > 0, item order) its score and the count of items scored strictly higher."""
+    labels = np.asarray(labels)
+    scores = np.asarray(scores)
+    pi = np.nonzero(labels > 0)[0]
+    above = np.array([np.count_nonzero(scores > scores[i]) for i in pi], np.int64)
+    return float(np.sum(scores * scores)), scores[pi], above

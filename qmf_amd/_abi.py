@@ -51,6 +51,8 @@ SIGNATURES = {
     "qmfx_bpr_epoch": [vp, c_u64, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_int, c_int],
     "qmfx_bpr_apply": [vp, P_i64, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_int],
     "qmfx_bpr_eval": [vp, c_int, P_i64, c_i64, c_int, P_f64],
+    "qmfx_eval_set_labels": [vp, c_i64, P_i64, P_i64, P_i64, P_f64],
+    "qmfx_eval_ranks": [vp, c_int, P_f64, P_i64, P_f64],
     "qmfx_rccl_unique_id": [P_u8],
     "qmfx_dist_init": [vp, c_int, c_int, P_u8],
     "qmfx_partition_rows": [P_i64, c_i64, c_int, c_int, P_i64, P_i64],
@@ -273,6 +275,27 @@ class Context:
         _check(lib().qmfx_bpr_eval(self.h, slot, _p(t, P_i64), len(t), int(use_biases),
                                    ctypes.byref(out)))
         return out.value
+
+    # ---- test-set evaluation (Engine.cpp:73-96, Metrics.cpp:27-164)
+    def eval_set_labels(self, users, rowptr, items, values):
+        """Test users (user idx) and their labelled items as a CSR over the test slots."""
+        users = np.ascontiguousarray(users, np.int64)
+        rowptr = np.ascontiguousarray(rowptr, np.int64)
+        items = np.ascontiguousarray(items, np.int64)
+        values = np.ascontiguousarray(values, np.float64)
+        if len(rowptr) != len(users) + 1 or len(items) != rowptr[-1] or len(values) != len(items):
+            raise QmfxError("label CSR shape mismatch")
+        _check(lib().qmfx_eval_set_labels(self.h, len(users), _p(users, P_i64), _p(rowptr, P_i64),
+                                          _p(items, P_i64), _p(values, P_f64)))
+        self._ev = (len(users), int(rowptr[-1]), int(np.count_nonzero(values > 0)))
+
+    def eval_ranks(self, use_biases=False):
+        """(label_scores, above, sq_sum): see include/qmfx.h qmfx_eval_ranks."""
+        nt, nl, npos = self._ev
+        ls, ab, sq = np.empty(nl), np.empty(npos, np.int64), np.empty(nt)
+        _check(lib().qmfx_eval_ranks(self.h, int(use_biases), _p(ls, P_f64), _p(ab, P_i64),
+                                     _p(sq, P_f64)))
+        return ls, ab, sq
 
     # ---- dist / stats
     def dist_init(self, rank, world, uid):

@@ -161,4 +161,31 @@ hipError_t launch_fill_uniform_f32(float* X, int64_t n, int kp, int k, double bo
 hipError_t launch_fill_uniform_f64(double* X, int64_t n, int kp, int k, double bound,
                                    uint64_t seed, hipStream_t s);
 
+// Test-set ranking statistics (eval.hip)
+template <typename T>
+struct EvalArgs {
+  const T* U;               // [nu][kp]
+  const T* I;               // [ni][kp]
+  const T* bias;            // [ni] item biases or nullptr
+  const int64_t* users;     // [ntest] test user rows
+  int64_t ntest;
+  int64_t nitems;
+  int k, kp;
+  // labelled (user, item) pairs, grouped by test slot
+  const int32_t* lab_slot;  // [nlab]
+  const int64_t* lab_item;  // [nlab]
+  const int64_t* lab_pidx;  // [nlab] index into the positives, or -1 (label <= 0)
+  int64_t nlab;
+  double* lab_score;        // [nlab] out
+  // positives (label > 0), grouped by test slot: pptr[t]..pptr[t+1]
+  const int64_t* pptr;      // [ntest + 1]
+  double* pscore;           // [npos] scores (written by the label pass)
+  unsigned long long* above;  // [npos] items scored strictly higher (zeroed by the caller)
+  double* sq_part;          // [eval_chunks(ntest, nitems)][ntest] Σ score² per item chunk
+  int64_t chunk;            // set by the launcher
+};
+int64_t eval_chunks(int64_t ntest, int64_t nitems);
+hipError_t launch_eval_ranks(const EvalArgs<float>& a, hipStream_t s);
+hipError_t launch_eval_ranks(const EvalArgs<double>& a, hipStream_t s);
+
 }  // namespace qmfx

@@ -111,6 +111,17 @@ struct qmfx_ctx {
   int64_t trip_n[2] = {0, 0};
   const void* trip_src[2] = {nullptr, nullptr};
   double* eval_partial = nullptr;
+  // test-set evaluation (qmfx_eval_set_labels / qmfx_eval_ranks)
+  int64_t ev_ntest = 0, ev_nlab = 0, ev_npos = 0, ev_chunks = 0;
+  int64_t* ev_users = nullptr;
+  int32_t* ev_slot = nullptr;
+  int64_t* ev_item = nullptr;
+  int64_t* ev_pidx = nullptr;
+  int64_t* ev_pptr = nullptr;
+  double* ev_lscore = nullptr;
+  double* ev_pscore = nullptr;
+  unsigned long long* ev_above = nullptr;
+  double* ev_sq = nullptr;
   uint64_t bpr_epochs = 0;
   int ablate = 0;  // QMFX_ABLATE (timing experiments only)
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
@@ -406,6 +417,15 @@ int qmfx_destroy(qmfx_ctx* c) {
   if (c->hsum) (void)hipHostFree(c->hsum);
   dfree_t(c->bad);
   dfree_t(c->eval_partial);
+  dfree_t(c->ev_users);
+  dfree_t(c->ev_slot);
+  dfree_t(c->ev_item);
+  dfree_t(c->ev_pidx);
+  dfree_t(c->ev_pptr);
+  dfree_t(c->ev_lscore);
+  dfree_t(c->ev_pscore);
+  dfree_t(c->ev_above);
+  dfree_t(c->ev_sq);
   dfree_t(c->pos_user);
   dfree_t(c->pos_item);
   dfree_t(c->urowptr);
@@ -1202,6 +1222,112 @@ int qmfx_bpr_eval(qmfx_ctx* c, int slot, const int64_t* trip, int64_t n, int use
   HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   *loss_sum = *c->hsum;
+  return 0;
+}
+
+// ---- test-set evaluation ---------------------------------------------------------------------
+int qmfx_eval_set_labels(qmfx_ctx* c, int64_t ntest, const int64_t* users, const int64_t* rowptr,
+                         const int64_t* items, const double* values) {
+  if (!c->s[0].F || !c->s[1].F) return fail("factors not allocated (qmfx_set_shape first)");
+  if (ntest < 0 || ntest > (int64_t)65535 * 16) return fail("ntest out of range");
+  if (c->k > 256) return fail("evaluation supports nfactors <= 256");
+  if (set_dev(c)) return -2;
+  const int64_t nu = c->s[0].n, ni = c->s[1].n;
+  if (ntest > 0 && rowptr[0] != 0) return fail("label rowptr must start at 0");
+  const int64_t nlab = ntest > 0 ? rowptr[ntest] : 0;
+  std::vector<int32_t> slot((size_t)nlab);
+  std::vector<int64_t> pidx((size_t)nlab), pptr((size_t)ntest + 1, 0);
+  int64_t np = 0;
+  for (int64_t t = 0; t < ntest; ++t) {
+    if (users[t] < 0 || users[t] >= nu) return fail("test user index out of range");
+    if (rowptr[t + 1] < rowptr[t]) return fail("label rowptr not ascending");
+    pptr[(size_t)t] = np;
+    for (int64_t e = rowptr[t]; e < rowptr[t + 1]; ++e) {
+      if (items[e] < 0 || items[e] >= ni) return fail("label item index out of range");
+      slot[(size_t)e] = (int32_t)t;
+      pidx[(size_t)e] = values[e] > 0.0 ? np++ : -1;
+    }
+  }
+  pptr[(size_t)ntest] = np;
+  const int64_t nch = eval_chunks(ntest, ni);
+  dfree_t(c->ev_users);
+  dfree_t(c->ev_slot);
+  dfree_t(c->ev_item);
+  dfree_t(c->ev_pidx);
+  dfree_t(c->ev_pptr);
+  dfree_t(c->ev_lscore);
+  dfree_t(c->ev_pscore);
+  dfree_t(c->ev_above);
+  dfree_t(c->ev_sq);
+  const size_t nl = (size_t)std::max<int64_t>(nlab, 1), npp = (size_t)std::max<int64_t>(np, 1);
+  HIPCHK(hipMalloc(&c->ev_users, (size_t)std::max<int64_t>(ntest, 1) * 8));
+  HIPCHK(hipMalloc(&c->ev_slot, nl * 4));
+  HIPCHK(hipMalloc(&c->ev_item, nl * 8));
+  HIPCHK(hipMalloc(&c->ev_pidx, nl * 8));
+  HIPCHK(hipMalloc(&c->ev_pptr, ((size_t)ntest + 1) * 8));
+  HIPCHK(hipMalloc(&c->ev_lscore, nl * 8));
+  HIPCHK(hipMalloc(&c->ev_pscore, npp * 8));
+  HIPCHK(hipMalloc(&c->ev_above, npp * 8));
+  HIPCHK(hipMalloc(&c->ev_sq, (size_t)std::max<int64_t>(nch * ntest, 1) * 8));
+  HIPCHK(scopy(c, c->ev_users, users, (size_t)ntest * 8, hipMemcpyHostToDevice));
+  HIPCHK(scopy(c, c->ev_slot, slot.data(), (size_t)nlab * 4, hipMemcpyHostToDevice));
+  HIPCHK(scopy(c, c->ev_item, items, (size_t)nlab * 8, hipMemcpyHostToDevice));
+  HIPCHK(scopy(c, c->ev_pidx, pidx.data(), (size_t)nlab * 8, hipMemcpyHostToDevice));
+  HIPCHK(scopy(c, c->ev_pptr, pptr.data(), pptr.size() * 8, hipMemcpyHostToDevice));
+  c->ev_ntest = ntest;
+  c->ev_nlab = nlab;
+  c->ev_npos = np;
+  c->ev_chunks = nch;
+  return 0;
+}
+
+}  // extern "C"
+
+template <typename T>
+static EvalArgs<T> eval_args(qmfx_ctx* c, int use_biases) {
+  EvalArgs<T> a{};
+  a.U = (const T*)c->s[0].F;
+  a.I = (const T*)c->s[1].F;
+  a.bias = use_biases ? (const T*)c->bias : nullptr;
+  a.users = c->ev_users;
+  a.ntest = c->ev_ntest;
+  a.nitems = c->s[1].n;
+  a.k = c->k;
+  a.kp = c->kp;
+  a.lab_slot = c->ev_slot;
+  a.lab_item = c->ev_item;
+  a.lab_pidx = c->ev_pidx;
+  a.nlab = c->ev_nlab;
+  a.lab_score = c->ev_lscore;
+  a.pptr = c->ev_pptr;
+  a.pscore = c->ev_pscore;
+  a.above = c->ev_above;
+  a.sq_part = c->ev_sq;
+  return a;
+}
+
+extern "C" {
+
+int qmfx_eval_ranks(qmfx_ctx* c, int use_biases, double* label_scores, int64_t* above,
+                    double* sq_sum) {
+  if (!c->ev_users) return fail("no test labels (qmfx_eval_set_labels first)");
+  if (use_biases && !c->bias) return fail("no item biases on the context");
+  if (set_dev(c)) return -2;
+  const int64_t nt = c->ev_ntest, nch = c->ev_chunks;
+  HIPCHK(hipMemsetAsync(c->ev_above, 0, (size_t)std::max<int64_t>(c->ev_npos, 1) * 8, c->stream));
+  if (c->prec == 32)
+    HIPCHK(launch_eval_ranks(eval_args<float>(c, use_biases), c->stream));
+  else
+    HIPCHK(launch_eval_ranks(eval_args<double>(c, use_biases), c->stream));
+  std::vector<double> part((size_t)(nch * nt));
+  HIPCHK(scopy(c, label_scores, c->ev_lscore, (size_t)c->ev_nlab * 8, hipMemcpyDeviceToHost));
+  HIPCHK(scopy(c, above, c->ev_above, (size_t)c->ev_npos * 8, hipMemcpyDeviceToHost));
+  HIPCHK(scopy(c, part.data(), c->ev_sq, part.size() * 8, hipMemcpyDeviceToHost));
+  for (int64_t t = 0; t < nt; ++t) {
+    double v = 0.0;
+    for (int64_t ch = 0; ch < nch; ++ch) v += part[(size_t)(ch * nt + t)];
+    sq_sum[t] = v;
+  }
   return 0;
 }
 

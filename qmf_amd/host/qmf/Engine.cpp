@@ -8,6 +8,7 @@
 #include <unordered_map>
 #include <unordered_set>
 
+#include <qmf/Device.h>
 #include <qmf/utils/Log.h>
 
 namespace qmf {
@@ -69,6 +70,54 @@ void Engine::computeTestScores(std::vector<std::vector<Double>>& testScores,
       scores[i] = s;
     }
   });
+}
+
+void Engine::computeTestRanks(qmfx_ctx* ctx, bool useBiases,
+                              const std::vector<size_t>& testUsers,
+                              const std::vector<std::vector<Double>>& testLabels,
+                              std::vector<RankedUser>& ranks) {
+  CHECK_EQ(testUsers.size(), testLabels.size());
+  const size_t nt = testUsers.size();
+  auto& L = testCsr_;
+  if (!L.uploaded) {
+    L.rowptr.assign(1, 0);
+    for (const auto& row : testLabels) {
+      for (size_t i = 0; i < row.size(); ++i)
+        if (row[i] != 0.0) {
+          L.items.push_back(static_cast<int64_t>(i));
+          L.values.push_back(row[i]);
+          L.npos += row[i] > 0.0;
+        }
+      L.rowptr.push_back(static_cast<int64_t>(L.items.size()));
+    }
+    const std::vector<int64_t> users(testUsers.begin(), testUsers.end());
+    QMFX_CHECK(qmfx_eval_set_labels(ctx, static_cast<int64_t>(nt), users.data(),
+                                    L.rowptr.data(), L.items.data(), L.values.data()));
+    L.uploaded = true;
+  }
+  std::vector<double> lscore(L.items.size()), sq(nt);
+  std::vector<int64_t> above(L.npos);
+  QMFX_CHECK(qmfx_eval_ranks(ctx, useBiases ? 1 : 0, lscore.data(), above.data(), sq.data()));
+  ranks.assign(nt, RankedUser());
+  size_t p = 0;
+  for (size_t t = 0; t < nt; ++t) {
+    RankedUser& r = ranks[t];
+    r.nitems = testLabels[t].size();
+    // Σ score² over all items, with the labelled items' terms swapped for (label − score)²
+    Double sse = sq[t];
+    std::vector<Double> ps;
+    std::vector<int64_t> ab;
+    for (int64_t e = L.rowptr[t]; e < L.rowptr[t + 1]; ++e) {
+      const Double l = L.values[e], s = lscore[e];
+      sse += (l - s) * (l - s) - s * s;
+      if (l > 0.0) {
+        ps.push_back(s);
+        ab.push_back(above[p++]);
+      }
+    }
+    r.sse = sse;
+    r.setPositives(ps, ab);
+  }
 }
 
 namespace {

@@ -8,9 +8,11 @@
 
 #include <qmf/DatasetReader.h>
 #include <qmf/FactorData.h>
+#include <qmf/metrics/Metrics.h>
 #include <qmf/Types.h>
 #include <qmf/utils/IdIndex.h>
 #include <qmf/utils/ParallelExecutor.h>
+#include <qmfx.h>
 
 namespace qmf {
 
@@ -49,12 +51,28 @@ class Engine {
                                 const FactorData& itemFactors,
                                 ParallelExecutor& parallel);
 
+  // Device evaluation (addition to the reference API): the same per-user metrics without the
+  // dense score matrix.  The non-zero test labels go to the device once (as a CSR over the
+  // test users); each call scores the context's current factors there and returns one
+  // RankedUser per test user (include/qmfx.h qmfx_eval_ranks).
+  void computeTestRanks(qmfx_ctx* ctx, bool useBiases, const std::vector<size_t>& testUsers,
+                        const std::vector<std::vector<Double>>& testLabels,
+                        std::vector<RankedUser>& ranks);
+
   // "<id>[ <bias>] <f0> ... <fk-1>\n" per idx, std::fixed with 9 decimals
   static void saveFactors(const FactorData& factorData, const IdIndex& index,
                           const std::string& fileName);
   static void saveFactors(const FactorData& factorData, const IdIndex& index, std::ostream& out);
 
   friend class EngineTestPeer;
+
+ private:
+  struct TestLabelCsr {
+    std::vector<int64_t> rowptr, items;
+    std::vector<Double> values;
+    size_t npos = 0;
+    bool uploaded = false;
+  } testCsr_;
 };
 
 }  // namespace qmf

@@ -187,9 +187,8 @@ void BPREngine::evaluate(const size_t epoch) {
             << ", test loss = " << lastTestLoss_;
   if (metricsEngine_ && !metricsEngine_->testAvgMetrics().empty() && !testUsers_.empty() &&
       (metricsEngine_->config().alwaysCompute || epoch == config_.nepochs)) {
-    syncHost();
-    computeTestScores(testScores_, testUsers_, *userFactors_, *itemFactors_, parallel_);
-    metricsEngine_->computeAndRecordTestAvgMetrics(epoch, testLabels_, testScores_, parallel_);
+    computeTestRanks(dev_->get(), itemFactors_->withBiases(), testUsers_, testLabels_, testRanks_);
+    metricsEngine_->computeAndRecordTestAvgMetrics(epoch, testRanks_, parallel_);
   }
 }
 

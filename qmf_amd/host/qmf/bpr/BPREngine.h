@@ -124,6 +124,7 @@ class BPREngine : public Engine {
   std::vector<size_t> testUsers_;
   std::vector<std::vector<Double>> testLabels_;
   std::vector<std::vector<Double>> testScores_;
+  std::vector<RankedUser> testRanks_;
 
   Double lastTrainLoss_ = -1.0;
   Double lastTestLoss_ = -1.0;

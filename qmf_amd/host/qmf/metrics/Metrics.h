@@ -9,11 +9,27 @@
 
 namespace qmf {
 
+// One test user's ranking over all nitems items, as reduced on the device
+// (qmfx_eval_ranks, csrc/eval.hip) instead of a dense score vector.  Every metric is a
+// function of these: the reference sorts (score, label > 0) pairs descending, so the
+// positives' places in that order are fixed by how many items score strictly higher.
+struct RankedUser {
+  size_t nitems = 0;
+  Double sse = 0.0;                 // Σ_i (label_i − score_i)² over all items
+  std::vector<int64_t> positions;   // 0-based places of the positives, ascending
+
+  // positives (label > 0) with their scores and the count of items scored strictly higher
+  void setPositives(const std::vector<Double>& scores, const std::vector<int64_t>& above);
+};
+
 class Metric {
  public:
   virtual ~Metric() = default;
   virtual Double compute(const std::vector<Double>& labels,
                          const std::vector<Double>& scores) const = 0;
+  // the same value from the device-reduced ranking (addition to the reference API)
+  virtual Double compute(const RankedUser& user) const = 0;
+  virtual Double compute(const std::vector<RankedUser>& users, ParallelExecutor& parallel) const;
   // mean over users
   virtual Double compute(const std::vector<std::vector<Double>>& labels,
                          const std::vector<std::vector<Double>>& scores) const;
@@ -27,6 +43,7 @@ class MeanSquaredError : public Metric {
   using Metric::compute;
   Double compute(const std::vector<Double>& labels,
                  const std::vector<Double>& scores) const override;
+  Double compute(const RankedUser& user) const override;
 };
 
 class AUC : public Metric {
@@ -34,6 +51,7 @@ class AUC : public Metric {
   using Metric::compute;
   Double compute(const std::vector<Double>& labels,
                  const std::vector<Double>& scores) const override;
+  Double compute(const RankedUser& user) const override;
 };
 
 class Precision : public Metric {
@@ -42,6 +60,7 @@ class Precision : public Metric {
   explicit Precision(const size_t k) : k_(k) {}
   Double compute(const std::vector<Double>& labels,
                  const std::vector<Double>& scores) const override;
+  Double compute(const RankedUser& user) const override;
 
  private:
   const size_t k_;
@@ -53,6 +72,7 @@ class Recall : public Metric {
   explicit Recall(const size_t k) : k_(k) {}
   Double compute(const std::vector<Double>& labels,
                  const std::vector<Double>& scores) const override;
+  Double compute(const RankedUser& user) const override;
 
  private:
   const size_t k_;
@@ -63,6 +83,7 @@ class AveragePrecision : public Metric {
   using Metric::compute;
   Double compute(const std::vector<Double>& labels,
                  const std::vector<Double>& scores) const override;
+  Double compute(const RankedUser& user) const override;
 };
 
 }  // namespace qmf

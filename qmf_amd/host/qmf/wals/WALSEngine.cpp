@@ -145,9 +145,8 @@ void WALSEngine::evaluate(const size_t epoch) {
   if (metricsEngine_ && !metricsEngine_->testAvgMetrics().empty() && !testUsers_.empty() &&
       (metricsEngine_->config().alwaysCompute || epoch == config_.nepochs)) {
     LOG(INFO) << "do compute evaluate ...";
-    syncHost();
-    computeTestScores(testScores_, testUsers_, *userFactors_, *itemFactors_, parallel_);
-    metricsEngine_->computeAndRecordTestAvgMetrics(epoch, testLabels_, testScores_, parallel_);
+    computeTestRanks(dev_->get(), false, testUsers_, testLabels_, testRanks_);
+    metricsEngine_->computeAndRecordTestAvgMetrics(epoch, testRanks_, parallel_);
   }
 }
 

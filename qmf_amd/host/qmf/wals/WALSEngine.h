@@ -87,6 +87,7 @@ class WALSEngine : public Engine {
   std::vector<size_t> testUsers_;
   std::vector<std::vector<Double>> testLabels_;
   std::vector<std::vector<Double>> testScores_;
+  std::vector<RankedUser> testRanks_;
 
   Double lastLoss_ = 0.0;
   size_t hostResolved_ = 0;

@@ -254,8 +254,28 @@ TEST(DatasetReader, parallelFileParseEqualsSequential) {
 }
 
 // ---- metrics (MetricsTest.cpp:23-87, MetricsManagerTest.cpp:23-44) -----------------------
+// The statistics qmfx_eval_ranks reduces on the device, formed here by brute force
+static RankedUser rankedOf(const std::vector<Double>& l, const std::vector<Double>& s) {
+  RankedUser r;
+  r.nitems = l.size();
+  std::vector<Double> ps;
+  std::vector<int64_t> ab;
+  for (size_t i = 0; i < l.size(); ++i) {
+    r.sse += (l[i] - s[i]) * (l[i] - s[i]);
+    if (l[i] > 0.0) {
+      ps.push_back(s[i]);
+      ab.push_back(std::count_if(s.begin(), s.end(), [&](Double x) { return x > s[i]; }));
+    }
+  }
+  r.setPositives(ps, ab);
+  return r;
+}
+
+// dense (reference) value; the ranked path must agree
 static Double one(const Metric& m, std::vector<Double> l, std::vector<Double> s) {
-  return m.compute(l, s);
+  const Double dense = m.compute(l, s);
+  EXPECT_NEAR(m.compute(rankedOf(l, s)), dense, 1e-12 * std::fabs(dense) + 1e-15);
+  return dense;
 }
 
 TEST(Metrics, knownAnswers) {
@@ -299,6 +319,40 @@ TEST(Metrics, knownAnswers) {
   EXPECT_DOUBLE_EQ(one(ap, {0.0, 1.0, 0.0}, {3.0, 1.0, 2.0}), 1.0 / 3);
   EXPECT_DEATH(one(ap, {0.0, 0.0}, {1.0, 2.0}));
   EXPECT_DEATH(one(p2, {1.0}, {1.0}));
+}
+
+// Ranked (device-statistics) metrics equal the dense ones, ties and negative labels included
+TEST(Metrics, rankedEqualsDense) {
+  std::mt19937 gen(7);
+  MeanSquaredError mse;
+  AUC auc;
+  AveragePrecision ap;
+  const Double labelSet[] = {-1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 2.0};
+  for (int trial = 0; trial < 400; ++trial) {
+    const size_t n = 1 + gen() % 60;
+    std::vector<Double> l(n), s(n);
+    for (size_t i = 0; i < n; ++i) {
+      l[i] = labelSet[gen() % 7];
+      s[i] = trial % 2 ? static_cast<Double>(gen() % 5) : std::ldexp(gen() % 100000, -7);
+    }
+    const bool anyPos = std::any_of(l.begin(), l.end(), [](Double x) { return x > 0.0; });
+    one(mse, l, s);
+    if (anyPos && std::any_of(l.begin(), l.end(), [](Double x) { return x <= 0.0; }))
+      one(auc, l, s);
+    if (anyPos) one(ap, l, s);
+    for (size_t k : {1, 2, 5, 10}) {
+      if (n < k) continue;
+      one(Precision(k), l, s);
+      if (anyPos) one(Recall(k), l, s);
+    }
+  }
+  // mean over users through the executor
+  std::vector<RankedUser> users = {rankedOf({1.0, 0.0}, {0.5, 0.5}),
+                                   rankedOf({1.0, 0.0, 1.0}, {0.0, 1.0, 2.0})};
+  ParallelExecutor px(2);
+  EXPECT_DOUBLE_EQ(mse.compute(users, px), 0.5 * (0.25 + 1.0));
+  EXPECT_DEATH(ap.compute(rankedOf({0.0, 0.0}, {1.0, 2.0})));
+  EXPECT_DEATH(Precision(2).compute(rankedOf({1.0}, {1.0})));
 }
 
 TEST(MetricsManager, parseAndExists) {

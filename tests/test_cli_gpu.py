@@ -123,24 +123,28 @@ def test_wals_cli_test_metrics(tmp_path):
     rec = dict(re.findall(r"recorded metric (\w+@?\d*) = ([-\d.e+]+)", log))
     assert set(rec) == {"test_avg_auc", "test_avg_p@5", "test_avg_r@10", "test_avg_ap",
                         "test_avg_mse"}
-    # AUC recomputed from the saved factors over every test user (numTestUsers = 0)
+    # every metric recomputed by the oracle (dense scores, Metrics.cpp restatement) from the
+    # saved factors over every test user (numTestUsers = 0); the saved files carry 9
+    # decimals, hence the tolerance
     uid, iid = o.ids(0), o.ids(1)
     L = {}
     for a, b, w in zip(*te):
         if a in set(uid) and b in set(iid):
             L.setdefault(int(np.searchsorted(uid, a)), {})[int(np.searchsorted(iid, b))] = w
-    aucs = []
-    S = U @ I.T
-    for uu, labs in L.items():
+    users = sorted(L)
+    S = po.test_scores(U, I, users)
+    vals = {"auc": [], "p@5": [], "r@10": [], "ap": [], "mse": []}
+    for t, uu in enumerate(users):
         lab = np.zeros(len(iid))
-        for it, w in labs.items():
+        for it, w in L[uu].items():
             lab[it] = w
-        pos, neg = S[uu][lab > 0], S[uu][lab <= 0]
-        if len(pos) == 0 or len(neg) == 0:
-            aucs.append(1.0)
-            continue
-        aucs.append(np.mean(pos[:, None] > neg[None, :]))
-    assert abs(float(rec["test_avg_auc"]) - np.mean(aucs)) < 1e-4
+        vals["auc"].append(po.metric_auc(lab, S[t]))
+        vals["p@5"].append(po.metric_precision(lab, S[t], 5))
+        vals["r@10"].append(po.metric_recall(lab, S[t], 10))
+        vals["ap"].append(po.metric_ap(lab, S[t]))
+        vals["mse"].append(po.metric_mse(lab, S[t]))
+    for name, v in vals.items():
+        assert abs(float(rec["test_avg_" + name]) - np.mean(v)) < 1e-4 * max(1.0, abs(np.mean(v))), name
 
 
 def clustered(nusers, nitems, nnz, seed, groups=10):
@@ -250,3 +254,40 @@ def test_bpr_cli_eval_losses_match_oracle(tmp_path, precision):
     for e, ((dtr, dte), (str_, ste)) in enumerate(zip(pairs, sim)):
         tol = 0.06 if e == 0 else 0.02
         assert abs(dtr - str_) < tol and abs(dte - ste) < tol, (e, pairs, sim)
+
+
+def test_bpr_cli_test_metrics_with_biases(tmp_path):
+    # bpr's evaluation adds the item biases (Engine.cpp:84-86); every test user sampled
+    # (num_test_users=0).  Oracle metrics from the saved factors (9 decimals).
+    u, i, _ = clustered(300, 120, 6000, seed=4)
+    data, test = str(tmp_path / "bpr.txt"), str(tmp_path / "test.txt")
+    write_dataset(data, u, i, np.ones(len(u)))
+    tu, ti, _ = clustered(300, 120, 900, seed=40)
+    write_dataset(test, tu, ti, np.ones(len(tu)))
+    uf, itf = str(tmp_path / "U"), str(tmp_path / "I")
+    log = run("bpr", "--train_dataset=" + data, "--test_dataset=" + test, "--nepochs=3",
+              "--nfactors=12", "--use_biases=true", "--init_distribution_bound=0.1",
+              "--test_avg_metrics=auc,p@5,ap,mse", "--seed=3", "--precision=64",
+              "--user_factors=" + uf, "--item_factors=" + itf)
+    rec = dict(re.findall(r"recorded metric (\w+@?\d*) = ([-\d.e+]+)", log))
+    assert set(rec) == {"test_avg_auc", "test_avg_p@5", "test_avg_ap", "test_avg_mse"}
+    ui, U = read_factors(uf)
+    ii, b, I = read_factors(itf, biases=True)
+    uix = {int(x): n for n, x in enumerate(ui)}   # file order = the engine's idx order
+    iix = {int(x): n for n, x in enumerate(ii)}
+    L = {}
+    for a, c in zip(tu, ti):
+        if int(a) in uix and int(c) in iix:
+            L.setdefault(uix[int(a)], {})[iix[int(c)]] = 1.0
+    users = sorted(L)
+    S = po.test_scores(U, I, users, b)
+    vals = {"auc": [], "p@5": [], "ap": [], "mse": []}
+    for t, uu in enumerate(users):
+        lab = np.zeros(len(ii))
+        lab[list(L[uu])] = 1.0
+        vals["auc"].append(po.metric_auc(lab, S[t]))
+        vals["p@5"].append(po.metric_precision(lab, S[t], 5))
+        vals["ap"].append(po.metric_ap(lab, S[t]))
+        vals["mse"].append(po.metric_mse(lab, S[t]))
+    for name, v in vals.items():
+        assert abs(float(rec["test_avg_" + name]) - np.mean(v)) < 1e-4 * max(1.0, abs(np.mean(v))), name
