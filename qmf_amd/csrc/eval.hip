@@ -9,10 +9,14 @@
 // and equal-scored positives are interchangeable.)  The device computes exactly those:
 //
 //   eval_label_kernel  one thread per labelled (user, item): its score;
-//   eval_rank_kernel   a tile of item rows staged through LDS, 16 test users per workgroup;
-//                      each lane scores one item for 4 users, accumulates Σ score², and
-//                      counts, per positive of those users, the items scored above it
-//                      (wave ballot + popcount into LDS counters, flushed once per chunk).
+//   eval_users_kernel  the test users' factor rows as doubles, [groups·32][k] (zero padded);
+//   eval_rank_kernel   a tile of item rows staged through LDS, 32 test users per workgroup;
+//                      each lane scores one item for the 8 users of its wave — their factor
+//                      values are wave-uniform, read through the scalar cache straight into
+//                      SGPR operands, so LDS only carries the item tile — accumulates Σ
+//                      score², and counts, per positive of those users, the items scored
+//                      above it (wave ballot + popcount into LDS counters, flushed once per
+//                      chunk).
 //
 // Scores are formed as the reference does — bias (or 0), then one rounded multiply and one
 // rounded add per factor in factor order, no fused multiply-add — so they equal the host's
@@ -25,12 +29,13 @@ namespace qmfx {
 namespace {
 
 constexpr int EV_TI = 64;               // items per tile (one per lane)
-constexpr int EV_UW = 4;                // test users per wave
+constexpr int EV_UW = 8;                // test users per wave
 constexpr int EV_W = 4;                 // waves per workgroup
 constexpr int EV_UG = EV_UW * EV_W;     // test users per workgroup
 constexpr int EV_KC = 64;               // factor columns per LDS stage
-constexpr int EV_CAP = 2048;            // positives of a workgroup counted in LDS
+constexpr int EV_CAP = 4096;            // positives of a workgroup counted in LDS
 constexpr int EV_KMAX = 256;
+constexpr int EV_TS = EV_KC + 2;        // tile row stride (even: 8-byte aligned pairs)
 
 #pragma clang fp contract(off)
 __device__ __forceinline__ double mul_add_rn(double s, double a, double b) {
@@ -54,23 +59,37 @@ __global__ __launch_bounds__(256) void eval_label_kernel(EvalArgs<T> a) {
 }
 
 template <typename T>
+__global__ __launch_bounds__(256) void eval_users_kernel(EvalArgs<T> a) {
+  // layout [t / 8][f][t % 8]: one wave's 8 users at factor f are 64 contiguous bytes
+  const int64_t t = blockIdx.x;
+  const T* u = a.U + (t < a.ntest ? a.users[t] * (int64_t)a.kp : 0);
+  double* o = a.udbl + (t / EV_UW) * a.k * EV_UW + (t % EV_UW);
+  for (int f = threadIdx.x; f < a.k; f += blockDim.x)
+    o[f * EV_UW] = t < a.ntest ? (double)u[f] : 0.0;
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void eval_rank_kernel(EvalArgs<T> a) {
-  __shared__ T tile[EV_TI][EV_KC + 1];
-  __shared__ double us[EV_UG][EV_KMAX];
+  __shared__ T tile[EV_TI * EV_TS];
   __shared__ uint32_t cnt[EV_CAP];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t t0 = (int64_t)blockIdx.y * EV_UG;
+  const int64_t tw = t0 + w * EV_UW;  // first user of this wave
   const int64_t i0 = (int64_t)blockIdx.x * a.chunk;
   const int64_t i1 = i0 + a.chunk < a.nitems ? i0 + a.chunk : a.nitems;
   const int64_t tl = t0 + EV_UG < a.ntest ? t0 + EV_UG : a.ntest;
-  const int64_t pb = a.pptr[t0], pe = a.pptr[tl];
+  const int64_t pb = a.pptr[t0], pe = a.pptr[tl];  // (scalar: kernel arguments only)
+  // wave-uniform rows, read through the constant address space so they become scalar loads
+  // (the kernel's own global stores would otherwise keep them on the vector path)
+  typedef const __attribute__((address_space(4))) double* cdptr;
+  const cdptr ud = (cdptr)(a.udbl + tw * a.k);  // [f][8] for this wave's users
+  const cdptr ps = (cdptr)a.pscore;  // written by eval_label_kernel (an earlier launch)
+  typedef const __attribute__((address_space(4))) int64_t* ciptr;
+  const ciptr pp = (ciptr)a.pptr;
 
   for (int x = threadIdx.x; x < EV_CAP; x += 256) cnt[x] = 0;
-  for (int x = threadIdx.x; x < EV_UG * a.k; x += 256) {
-    const int g = x / a.k, f = x - g * a.k;
-    us[g][f] = t0 + g < a.ntest ? (double)a.U[a.users[t0 + g] * (int64_t)a.kp + f] : 0.0;
-  }
 
   double sq[EV_UW];
 #pragma unroll
@@ -88,32 +107,51 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(EvalArgs<T> a) {
       __syncthreads();
       for (int x = threadIdx.x; x < EV_TI * EV_KC; x += 256) {
         const int r = x / EV_KC, cc = x - r * EV_KC;
-        tile[r][cc] = (ib + r < i1 && cc < kc) ? a.I[(ib + r) * a.kp + f0 + cc] : (T)0;
+        tile[r * EV_TS + cc] = (ib + r < i1 && cc < kc) ? a.I[(ib + r) * a.kp + f0 + cc] : (T)0;
       }
       __syncthreads();
-      const double* u0 = &us[w * EV_UW][f0];
-#pragma unroll 4
-      for (int f = 0; f < kc; ++f) {
-        const double q = (double)tile[lane][f];
+      const T* q = &tile[lane * EV_TS];
+      const cdptr u0 = ud + f0 * EV_UW;
+      if (kc == EV_KC) {
+        // full stage, fully unrolled: every user value is an s_load at an immediate offset
 #pragma unroll
-        for (int g = 0; g < EV_UW; ++g) acc[g] = mul_add_rn(acc[g], u0[g * EV_KMAX + f], q);
+        for (int f = 0; f < EV_KC; ++f) {
+          const double qf = (double)q[f];
+#pragma unroll
+          for (int g = 0; g < EV_UW; ++g) acc[g] = mul_add_rn(acc[g], u0[f * EV_UW + g], qf);
+        }
+      } else {
+        for (int f = 0; f < kc; ++f) {
+          const double qf = (double)q[f];
+#pragma unroll
+          for (int g = 0; g < EV_UW; ++g) acc[g] = mul_add_rn(acc[g], u0[f * EV_UW + g], qf);
+        }
       }
     }
 #pragma unroll
     for (int g = 0; g < EV_UW; ++g) {
-      const int64_t t = t0 + w * EV_UW + g;
+      const int64_t t = tw + g;
       if (t >= a.ntest) break;  // uniform over the wave
       const double s = acc[g];
       if (valid) sq[g] += s * s;
-      const int64_t qb = a.pptr[t], qe = a.pptr[t + 1];
-      for (int64_t p = qb; p < qe; ++p) {
-        const uint64_t m = __ballot(valid && s > a.pscore[p]);
-        if (lane == 0 && m) {
-          const uint32_t c = (uint32_t)__popcll(m);
-          if (p - pb < EV_CAP)
-            atomicAdd(&cnt[p - pb], c);
-          else
-            atomicAdd((unsigned long long*)&a.above[p], (unsigned long long)c);
+      const int64_t qb = pp[t], qe = pp[t + 1];
+      // positives' scores through the scalar cache, four at a time
+      for (int64_t p0 = qb; p0 < qe; p0 += 4) {
+        double sp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sp[j] = p0 + j < qe ? ps[p0 + j] : 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t p = p0 + j;
+          if (p >= qe) break;
+          const uint64_t m = __ballot(valid && s > sp[j]);
+          if (lane == 0 && m) {
+            const uint32_t c = (uint32_t)__popcll(m);
+            if (p - pb < EV_CAP)
+              atomicAdd(&cnt[p - pb], c);
+            else
+              atomicAdd((unsigned long long*)&a.above[p], (unsigned long long)c);
+          }
         }
       }
     }
@@ -122,7 +160,7 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(EvalArgs<T> a) {
   // Σ score² of each user over this chunk: fixed-order wave sum, one slot per (chunk, user)
 #pragma unroll
   for (int g = 0; g < EV_UW; ++g) {
-    const int64_t t = t0 + w * EV_UW + g;
+    const int64_t t = tw + g;
     const double v = wave_sum(sq[g]);
     if (lane == 0 && t < a.ntest) a.sq_part[(int64_t)blockIdx.x * a.ntest + t] = v;
   }
@@ -142,6 +180,7 @@ hipError_t eval_ranks(const EvalArgs<T>& a0, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a.ntest == 0 || a.nitems == 0) return e;
   const int64_t groups = (a.ntest + EV_UG - 1) / EV_UG;
+  hipLaunchKernelGGL(eval_users_kernel<T>, dim3((unsigned)(groups * EV_UG)), dim3(256), 0, s, a);
   const int64_t nchunk = eval_chunks(a.ntest, a.nitems);
   a.chunk = ((a.nitems + nchunk - 1) / nchunk + EV_TI - 1) / EV_TI * EV_TI;
   if (groups > 65535) return hipErrorInvalidValue;
@@ -151,6 +190,8 @@ hipError_t eval_ranks(const EvalArgs<T>& a0, hipStream_t s) {
 }
 
 }  // namespace
+
+int64_t eval_user_rows(int64_t ntest) { return (ntest + EV_UG - 1) / EV_UG * EV_UG; }
 
 // Item chunks per user group: about 4096 workgroups over the grid, ≥ one tile per chunk.
 // The host sizes the Σ score² partial buffer [chunks][ntest] with the same function.

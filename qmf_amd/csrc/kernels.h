@@ -182,9 +182,11 @@ struct EvalArgs {
   double* pscore;           // [npos] scores (written by the label pass)
   unsigned long long* above;  // [npos] items scored strictly higher (zeroed by the caller)
   double* sq_part;          // [eval_chunks(ntest, nitems)][ntest] Σ score² per item chunk
+  double* udbl;             // [eval_user_rows(ntest)][k] scratch: test users' rows as doubles
   int64_t chunk;            // set by the launcher
 };
 int64_t eval_chunks(int64_t ntest, int64_t nitems);
+int64_t eval_user_rows(int64_t ntest);
 hipError_t launch_eval_ranks(const EvalArgs<float>& a, hipStream_t s);
 hipError_t launch_eval_ranks(const EvalArgs<double>& a, hipStream_t s);
 

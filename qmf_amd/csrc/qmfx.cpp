@@ -122,6 +122,7 @@ struct qmfx_ctx {
   double* ev_pscore = nullptr;
   unsigned long long* ev_above = nullptr;
   double* ev_sq = nullptr;
+  double* ev_udbl = nullptr;
   uint64_t bpr_epochs = 0;
   int ablate = 0;  // QMFX_ABLATE (timing experiments only)
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
@@ -426,6 +427,7 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree_t(c->ev_pscore);
   dfree_t(c->ev_above);
   dfree_t(c->ev_sq);
+  dfree_t(c->ev_udbl);
   dfree_t(c->pos_user);
   dfree_t(c->pos_item);
   dfree_t(c->urowptr);
@@ -1259,6 +1261,7 @@ int qmfx_eval_set_labels(qmfx_ctx* c, int64_t ntest, const int64_t* users, const
   dfree_t(c->ev_pscore);
   dfree_t(c->ev_above);
   dfree_t(c->ev_sq);
+  dfree_t(c->ev_udbl);
   const size_t nl = (size_t)std::max<int64_t>(nlab, 1), npp = (size_t)std::max<int64_t>(np, 1);
   HIPCHK(hipMalloc(&c->ev_users, (size_t)std::max<int64_t>(ntest, 1) * 8));
   HIPCHK(hipMalloc(&c->ev_slot, nl * 4));
@@ -1269,6 +1272,7 @@ int qmfx_eval_set_labels(qmfx_ctx* c, int64_t ntest, const int64_t* users, const
   HIPCHK(hipMalloc(&c->ev_pscore, npp * 8));
   HIPCHK(hipMalloc(&c->ev_above, npp * 8));
   HIPCHK(hipMalloc(&c->ev_sq, (size_t)std::max<int64_t>(nch * ntest, 1) * 8));
+  HIPCHK(hipMalloc(&c->ev_udbl, (size_t)std::max<int64_t>(eval_user_rows(ntest) * c->k, 1) * 8));
   HIPCHK(scopy(c, c->ev_users, users, (size_t)ntest * 8, hipMemcpyHostToDevice));
   HIPCHK(scopy(c, c->ev_slot, slot.data(), (size_t)nlab * 4, hipMemcpyHostToDevice));
   HIPCHK(scopy(c, c->ev_item, items, (size_t)nlab * 8, hipMemcpyHostToDevice));
@@ -1303,6 +1307,7 @@ static EvalArgs<T> eval_args(qmfx_ctx* c, int use_biases) {
   a.pscore = c->ev_pscore;
   a.above = c->ev_above;
   a.sq_part = c->ev_sq;
+  a.udbl = c->ev_udbl;
   return a;
 }
 

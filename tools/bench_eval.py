@@ -14,7 +14,8 @@ import qmf_amd  # noqa: E402
 
 
 def main():
-    nu, ni, k, nt, npos = 100_000, 1_000_000, 128, 1000, 10
+    nu, ni, k, nt = 100_000, 1_000_000, 128, 1000
+    npos = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     rng = np.random.default_rng(0)
     users = rng.choice(nu, nt, replace=False)
     items = np.concatenate([np.sort(rng.choice(ni, npos, replace=False)) for _ in range(nt)])

@@ -8,6 +8,7 @@ import sys
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name) if not name.startswith("void rocprim") else "rocprim::" + \
         (re.search(r"detail::(\w+)", name).group(1) if re.search(r"detail::(\w+)", name) else "kernel")
     return name.replace("void ", "")
