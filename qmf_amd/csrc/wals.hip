@@ -632,8 +632,13 @@ __global__ void gimg_kernel(const T* G, int k, double lambda, T* img) {
 // and the HBM traffic per signal is one gathered row, as in the direct kernel.
 // Writes x' (whitened); whiten_kernel<UNWHITEN> maps it to x = L⁻ᵀ x' and adds −λ‖x‖².
 // ---------------------------------------------------------------------------------------
+// minimum waves per SIMD of the NTN = 4 tiling (timing experiments: 1 lifts the 256-VGPR cap)
+#ifndef QMFX_WB4_MIN_WAVES
+#define QMFX_WB4_MIN_WAVES 2
+#endif
 template <typename T, int NTK, int NTN, bool TRACE>
-__global__ __launch_bounds__(64, NTK > 8 ? 1 : 2) void wals_woodbury_kernel(SolveArgs<T> a) {
+__global__ __launch_bounds__(64, NTK > 8 ? 1 : (NTN == 4 ? QMFX_WB4_MIN_WAVES : 2))
+void wals_woodbury_kernel(SolveArgs<T> a) {
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   using v4 = typename M::acc_t;  // 4-wide vector of T

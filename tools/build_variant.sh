@@ -5,5 +5,6 @@ set -e
 cd "$(dirname "$0")/../qmf_amd"
 B=_build
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fno-slp-vectorize $2 -c csrc/wals.hip -o $B/var_$1_wals.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $B/var_$1.so $B/var_$1_wals.o $B/wals_big.o $B/bpr.o $B/data.o $B/qmfx.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+OTHERS=$(ls $B/*.o | grep -v -e '/wals.o$' -e '/var_')
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $B/var_$1.so $B/var_$1_wals.o $OTHERS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f $B/var_$1_wals.o
