@@ -16,6 +16,8 @@
 //   * backward solve by 16-blocks: owners of L(J, I) tiles add their part of Lᵀx in LDS,
 //     wave 0 finishes the block with the diagonal triangle.
 // Same results contract as the single-wave kernels: status[row] = 1 on a non-positive pivot.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "rowsolve.h"
@@ -123,6 +125,31 @@ __device__ void big_panel(BigShared<T, NT>& S, int p, int lane, int& bad) {
   (void)cl;
 }
 
+// One 4-signal step of the Gram for the tiles of wave W (t = W + NW·s, compile-time map):
+// the wave reads each 16-row fragment of the staged signals once (NT LDS reads instead of
+// two per tile) and reuses it for every tile in its tile row or column.
+template <typename T, int NT, int W>
+__device__ __forceinline__ void big_gram_step(typename Mfma<T>::acc_t* acc, const T* yk, T wk) {
+  using C = BigCfg<T, NT>;
+  using M = Mfma<T>;
+  T y[NT], wy[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) {
+    y[J] = yk[16 * J];
+    wy[J] = wk * y[J];
+  }
+#pragma unroll
+  for (int s = 0; s < C::TPW; ++s) {
+    const int t = W + C::NW * s;
+    if (t < C::NTT) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const int J = t - I * (I + 1) / 2;
+      acc[s] = M::mma(y[I], wy[J], acc[s]);
+    }
+  }
+}
+
 template <typename T, int NT>
 __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
   using C = BigCfg<T, NT>;
@@ -224,18 +251,22 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       }
       // MFMAs of stage st: 4 signals per step, operands straight from LDS
       const T* sg = S.stage[buf];
+      auto gram_stage = [&](auto wtag) {
+        constexpr int W = decltype(wtag)::value;
 #pragma unroll 2
-      for (int k4 = 0; k4 < SIG; k4 += 4) {
-        const T* yk = sg + (k4 + kk) * KP + cl;
-        const T wk = S.w[buf][k4 + kk];
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-          if (TI[s] >= 0) {
-            const T ya = yk[16 * TI[s]];
-            const T yb = wk * yk[16 * TJ[s]];
-            acc[s] = M::mma(ya, yb, acc[s]);
-          }
-        }
+        for (int k4 = 0; k4 < SIG; k4 += 4)
+          big_gram_step<T, NT, W>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk]);
+      };
+      static_assert(NW == 4 || NW == 8, "wave count");
+      switch (wv) {
+        case 0: gram_stage(std::integral_constant<int, 0>{}); break;
+        case 1: gram_stage(std::integral_constant<int, 1>{}); break;
+        case 2: gram_stage(std::integral_constant<int, 2>{}); break;
+        case 3: gram_stage(std::integral_constant<int, 3>{}); break;
+        case 4: gram_stage(std::integral_constant<int, 4 % NW>{}); break;
+        case 5: gram_stage(std::integral_constant<int, 5 % NW>{}); break;
+        case 6: gram_stage(std::integral_constant<int, 6 % NW>{}); break;
+        default: gram_stage(std::integral_constant<int, 7 % NW>{}); break;
       }
       if (tid < KP) {
 #pragma unroll 4
