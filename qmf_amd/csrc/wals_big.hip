@@ -37,6 +37,9 @@ struct BigCfg {
   static constexpr int CPR = KP / VEC;                   // 16-B chunks per row
   static constexpr int TRIPS = (SIG * CPR + NTHR - 1) / NTHR;
   static constexpr int PLD = 17;                         // padded LDS row of a panel
+  // compile-time tile map with LDS fragments reused across a wave's tiles (Gram and
+  // trailing update); the fp64 tilings above NT = 11 lack the registers for it
+  static constexpr bool REUSE = sizeof(T) == 4 || NT <= 11;
 };
 
 template <typename T, int NT>
@@ -150,6 +153,38 @@ __device__ __forceinline__ void big_gram_step(typename Mfma<T>::acc_t* acc, cons
   }
 }
 
+// Rank-16 trailing update of panel p for the tiles of wave W (compile-time map): the panel
+// rows of every block I > p are read from LDS once (4 fragments each) and reused by all of
+// the wave's tiles in block row or column I.
+template <typename T, int NT, int W>
+__device__ __forceinline__ void big_trailing(typename Mfma<T>::acc_t* acc, const T* panel, int p,
+                                             int cl, int kk) {
+  using C = BigCfg<T, NT>;
+  using M = Mfma<T>;
+  T fr[NT][4];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) {
+    if (I > p) {
+      const T* src = panel + (16 * (I - p) + cl) * C::PLD + kk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fr[I][q] = src[4 * q];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < C::TPW; ++s) {
+    const int t = W + C::NW * s;
+    if (t < C::NTT) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const int J = t - I * (I + 1) / 2;
+      if (J > p) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[s] = M::mma(-fr[I][q], fr[J][q], acc[s]);
+      }
+    }
+  }
+}
+
 template <typename T, int NT>
 __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
   using C = BigCfg<T, NT>;
@@ -258,15 +293,27 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
           big_gram_step<T, NT, W>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk]);
       };
       static_assert(NW == 4 || NW == 8, "wave count");
-      switch (wv) {
-        case 0: gram_stage(std::integral_constant<int, 0>{}); break;
-        case 1: gram_stage(std::integral_constant<int, 1>{}); break;
-        case 2: gram_stage(std::integral_constant<int, 2>{}); break;
-        case 3: gram_stage(std::integral_constant<int, 3>{}); break;
-        case 4: gram_stage(std::integral_constant<int, 4 % NW>{}); break;
-        case 5: gram_stage(std::integral_constant<int, 5 % NW>{}); break;
-        case 6: gram_stage(std::integral_constant<int, 6 % NW>{}); break;
-        default: gram_stage(std::integral_constant<int, 7 % NW>{}); break;
+      if constexpr (C::REUSE) {
+        switch (wv) {
+          case 0: gram_stage(std::integral_constant<int, 0>{}); break;
+          case 1: gram_stage(std::integral_constant<int, 1>{}); break;
+          case 2: gram_stage(std::integral_constant<int, 2>{}); break;
+          case 3: gram_stage(std::integral_constant<int, 3>{}); break;
+          case 4: gram_stage(std::integral_constant<int, 4 % NW>{}); break;
+          case 5: gram_stage(std::integral_constant<int, 5 % NW>{}); break;
+          case 6: gram_stage(std::integral_constant<int, 6 % NW>{}); break;
+          default: gram_stage(std::integral_constant<int, 7 % NW>{}); break;
+        }
+      } else {
+#pragma unroll 2
+        for (int k4 = 0; k4 < SIG; k4 += 4) {
+          const T* yk = sg + (k4 + kk) * KP + cl;
+          const T wk = S.w[buf][k4 + kk];
+#pragma unroll
+          for (int s = 0; s < TPW; ++s) {
+            if (TI[s] >= 0) acc[s] = M::mma(yk[16 * TI[s]], wk * yk[16 * TJ[s]], acc[s]);
+          }
+        }
       }
       if (tid < KP) {
 #pragma unroll 4
@@ -308,11 +355,31 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           acc[s][r] = S.panel[(16 * (TI[s] - p) + M::crow(lane, r)) * PLD + cl];
-      } else if (TJ[s] > p && !(a.ablate & 4)) {
-        const T* li = S.panel + (16 * (TI[s] - p) + cl) * PLD + kk;
-        const T* lj = S.panel + (16 * (TJ[s] - p) + cl) * PLD + kk;
+      }
+    }
+    if constexpr (!C::REUSE) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[s] = M::mma(-li[4 * q], lj[4 * q], acc[s]);
+      for (int s = 0; s < TPW; ++s) {
+        if (TJ[s] > p && !(a.ablate & 4)) {
+          const T* li = S.panel + (16 * (TI[s] - p) + cl) * PLD + kk;
+          const T* lj = S.panel + (16 * (TJ[s] - p) + cl) * PLD + kk;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[s] = M::mma(-li[4 * q], lj[4 * q], acc[s]);
+        }
+      }
+    } else if (!(a.ablate & 4) && p + 1 < NT) {
+      auto trailing = [&](auto wtag) {
+        big_trailing<T, NT, decltype(wtag)::value>(acc, S.panel, p, cl, kk);
+      };
+      switch (wv) {
+        case 0: trailing(std::integral_constant<int, 0>{}); break;
+        case 1: trailing(std::integral_constant<int, 1>{}); break;
+        case 2: trailing(std::integral_constant<int, 2>{}); break;
+        case 3: trailing(std::integral_constant<int, 3>{}); break;
+        case 4: trailing(std::integral_constant<int, 4 % NW>{}); break;
+        case 5: trailing(std::integral_constant<int, 5 % NW>{}); break;
+        case 6: trailing(std::integral_constant<int, 6 % NW>{}); break;
+        default: trailing(std::integral_constant<int, 7 % NW>{}); break;
       }
     }
     __syncthreads();
