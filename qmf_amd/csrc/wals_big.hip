@@ -435,44 +435,86 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   }
 }
 
-// ---- YᵀY for large NT: one block row I of the lower triangle per blockIdx.y ---------------
+// ---- YᵀY for large NT, every tile per workgroup: the block's rows are staged through LDS
+// SIG at a time with coalesced 16-B loads, so Y is read from HBM once (a strip per block
+// row read it NT times: 42 -> 4 ms per launch at C5), and the waves split the NT(NT+1)/2
+// tiles as in the row kernel's Gram (big_gram_step, weight 1).
 template <typename T, int NT>
-__global__ __launch_bounds__(64) void gram_strip_kernel(const T* Y, int64_t n,
-                                                        int64_t rows_per_block,
-                                                        double* partial) {
+__global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void gram_tiles_kernel(
+    const T* Y, int64_t n, int64_t rows_per_block, double* partial) {
+  using C = BigCfg<T, NT>;
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
-  constexpr int KP = 16 * NT;
-  constexpr int NTT = NT * (NT + 1) / 2;
-  const int I = blockIdx.y;
-  const int lane = threadIdx.x;
+  using vec_t = T __attribute__((ext_vector_type(C::VEC)));
+  constexpr int KP = C::KP, NW = C::NW, TPW = C::TPW, NTT = C::NTT, SIG = C::SIG;
+  constexpr int CPR = C::CPR, TRIPS = C::TRIPS;
+  __shared__ __attribute__((aligned(16))) T stage[SIG * KP];
+
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
-  acc_t acc[NT];
+
+  int TI[TPW], TJ[TPW];
+  acc_t acc[TPW];
 #pragma unroll
-  for (int J = 0; J < NT; ++J) acc[J] = acc_t{0, 0, 0, 0};
-  for (int64_t e0 = r0; e0 < r1; e0 += 4) {
-    const int64_t e = e0 + kk;
-    const bool valid = e < r1;
-    const T* yrow = Y + (valid ? e : r0) * KP + cl;
-    const T ya = valid ? yrow[16 * I] : T(0);
+  for (int s = 0; s < TPW; ++s) {
+    const int t = wv + NW * s;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    TI[s] = t < NTT ? I : -1;
+    TJ[s] = t < NTT ? t - I * (I + 1) / 2 : -1;
+    acc[s] = acc_t{0, 0, 0, 0};
+  }
+
+  for (int64_t e0 = r0; e0 < r1; e0 += SIG) {
+    __syncthreads();
 #pragma unroll
-    for (int J = 0; J < NT; ++J) {
-      if (J <= I) {
-        const T yb = valid ? yrow[16 * J] : T(0);
-        acc[J] = M::mma(ya, yb, acc[J]);
+    for (int t = 0; t < TRIPS; ++t) {
+      const int ch = tid + C::NTHR * t;
+      if (ch < SIG * CPR) {
+        const int64_t e = e0 + ch / CPR;
+        const vec_t v = e < r1 ? *(reinterpret_cast<const vec_t*>(Y + e * KP) + ch % CPR)
+                               : vec_t{};
+        reinterpret_cast<vec_t*>(stage)[ch] = v;
+      }
+    }
+    __syncthreads();
+    if constexpr (C::REUSE) {
+      auto step = [&](auto wtag) {
+#pragma unroll 2
+        for (int k4 = 0; k4 < SIG; k4 += 4)
+          big_gram_step<T, NT, decltype(wtag)::value>(acc, stage + (k4 + kk) * KP + cl, T(1));
+      };
+      switch (wv) {
+        case 0: step(std::integral_constant<int, 0>{}); break;
+        case 1: step(std::integral_constant<int, 1>{}); break;
+        case 2: step(std::integral_constant<int, 2>{}); break;
+        case 3: step(std::integral_constant<int, 3>{}); break;
+        case 4: step(std::integral_constant<int, 4 % NW>{}); break;
+        case 5: step(std::integral_constant<int, 5 % NW>{}); break;
+        case 6: step(std::integral_constant<int, 6 % NW>{}); break;
+        default: step(std::integral_constant<int, 7 % NW>{}); break;
+      }
+    } else {
+      for (int k4 = 0; k4 < SIG; k4 += 4) {
+        const T* yk = stage + (k4 + kk) * KP + cl;
+#pragma unroll
+        for (int s = 0; s < TPW; ++s)
+          if (TI[s] >= 0) acc[s] = M::mma(yk[16 * TI[s]], yk[16 * TJ[s]], acc[s]);
       }
     }
   }
   double* out = partial + (int64_t)blockIdx.x * NTT * 256;
 #pragma unroll
-  for (int J = 0; J < NT; ++J) {
-    if (J <= I) {
-      const int t = tile_index(I, J);
+  for (int s = 0; s < TPW; ++s) {
+    if (TI[s] >= 0) {
+      const int t = tile_index(TI[s], TJ[s]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[t * 256 + M::crow(lane, r) * 16 + cl] = (double)acc[J][r];
+      for (int r = 0; r < 4; ++r) out[t * 256 + M::crow(lane, r) * 16 + cl] = (double)acc[s][r];
     }
   }
 }
@@ -503,11 +545,11 @@ static hipError_t launch_big_nt(const SolveArgs<T>& a, hipStream_t s) {
 }
 
 template <typename T, int NT>
-static hipError_t launch_gram_strip_nt(const T* Y, int64_t n, double* partial, int nblocks,
+static hipError_t launch_gram_tiles_nt(const T* Y, int64_t n, double* partial, int nblocks,
                                        int64_t rows_per_block, hipStream_t s) {
   if (nblocks > 0)
-    hipLaunchKernelGGL((gram_strip_kernel<T, NT>), dim3(nblocks, NT), dim3(64), 0, s, Y, n,
-                       rows_per_block, partial);
+    hipLaunchKernelGGL((gram_tiles_kernel<T, NT>), dim3(nblocks), dim3(BigCfg<T, NT>::NTHR), 0,
+                       s, Y, n, rows_per_block, partial);
   return hipGetLastError();
 }
 
@@ -546,7 +588,7 @@ static hipError_t gram_big(const T* Y, int64_t n, int nt, T* G, double* partial,
   if (rpb < 64) rpb = 64;
   const int nblocks = (int)((n + rpb - 1) / rpb);
   hipError_t e = hipSuccess;
-#define CALL(N) launch_gram_strip_nt<T, N>(Y, n, partial, nblocks, rpb, s)
+#define CALL(N) launch_gram_tiles_nt<T, N>(Y, n, partial, nblocks, rpb, s)
   e = [&]() -> hipError_t { QMFX_BIG_SWITCH(nt, CALL) }();
 #undef CALL
   if (e != hipSuccess) return e;
