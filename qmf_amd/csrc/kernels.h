@@ -65,7 +65,7 @@ hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* im
 
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s);
-// multi-wave row solve and strip YᵀY for large factor counts (wals_big.hip; nt 5..16)
+// multi-wave row solve and tiled YᵀY for large factor counts (wals_big.hip; nt 5..16)
 hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_big(const SolveArgs<double>& a, int nt, hipStream_t s);
 hipError_t launch_gram_big(const float* Y, int64_t n, int nt, float* G, double* partial,

@@ -225,7 +225,7 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 // Largest whitened-row bucket (NTN) usable for this factor tiling: n padded to 16 must be
 // at most 64 and at most KP/2 (beyond that the k×k solve is the cheaper one).
 // Factor counts beyond one wave's registers (fp32 k > 128, fp64 k > 64) use the multi-wave
-// row kernel and the strip YᵀY (wals_big.hip).
+// row kernel and the tiled YᵀY (wals_big.hip).
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
 
 int max_whitened_ntn(const qmfx_ctx* c) {
