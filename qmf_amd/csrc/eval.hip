@@ -33,7 +33,7 @@ constexpr int EV_UW = 8;                // test users per wave
 constexpr int EV_W = 4;                 // waves per workgroup
 constexpr int EV_UG = EV_UW * EV_W;     // test users per workgroup
 constexpr int EV_KC = 64;               // factor columns per LDS stage
-constexpr int EV_CAP = 4096;            // positives of a workgroup counted in LDS
+constexpr int EV_CAP = 2048;            // positives of a workgroup counted in LDS
 constexpr int EV_KMAX = 256;
 constexpr int EV_TS = EV_KC + 2;        // tile row stride (even: 8-byte aligned pairs)
 
