@@ -129,7 +129,7 @@ def partition_rows(rowptr, world, rank):
 class Context:
     """One device context (one GPU).  Mirrors the device state of a WALSEngine/BPREngine."""
 
-    def __init__(self, nfactors, precision=32, device=0):
+    def __init__(self, nfactors, precision=64, device=0):
         L = lib()
         h = vp()
         _check(L.qmfx_create(ctypes.byref(h), device, precision, nfactors))

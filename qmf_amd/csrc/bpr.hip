@@ -47,6 +47,16 @@ __device__ __forceinline__ void store_row(const Row<T, E>& r, T* base, int lane,
   for (int e = 0; e < E; ++e)
     if (lane + 64 * e < kp) st_shared(base + lane + 64 * e, r.v[e]);
 }
+// Adds (r − r0) to the shared row with L2 atomics: a concurrent wave's update of the same row
+// is kept instead of being overwritten (Hogwild without lost updates; the C4 "wavefront-atomic"
+// SGD).  Only the read that formed the gradient can be stale, as in the reference's threads.
+template <typename T, int E>
+__device__ __forceinline__ void add_row(const Row<T, E>& r, const Row<T, E>& r0, T* base,
+                                        int lane, int kp) {
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (lane + 64 * e < kp) unsafeAtomicAdd(base + lane + 64 * e, r.v[e] - r0.v[e]);
+}
 
 // One SGD step on (u, p, n).  Returns false if the derivative was not finite.
 template <typename T, int E>
@@ -71,21 +81,27 @@ __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t
   const T eg = T(1) / (T(1) + ex);
   if (!isfinite(eg)) return false;
   const T lr = a.lr;
+  // p == n (possible only in a caller-given sequence: sampled negatives are never positives):
+  // the reference updates q_n in place after q_p, so q_n's step starts from the new q_p
+  const bool same = p == n;
   if (a.use_biases && lane == 0) {
-    st_shared(a.bias + p, bp + lr * (eg - a.bias_lambda * bp));
-    st_shared(a.bias + n, bn + lr * (-eg - a.bias_lambda * bn));
+    const T bp_new = bp + lr * (eg - a.bias_lambda * bp);
+    const T bn_old = same ? bp_new : bn;
+    st_shared(a.bias + p, bp_new);
+    st_shared(a.bias + n, bn_old + lr * (-eg - a.bias_lambda * bn_old));
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const T pu_new = pu.v[e] + lr * (eg * (qp.v[e] - qn.v[e]) - a.user_lambda * pu.v[e]);
     const T qp_new = qp.v[e] + lr * (eg * pu_new - a.item_lambda * qp.v[e]);
-    const T qn_new = qn.v[e] + lr * (-eg * pu_new - a.item_lambda * qn.v[e]);
+    const T qn_old = same ? qp_new : qn.v[e];
+    const T qn_new = qn_old + lr * (-eg * pu_new - a.item_lambda * qn_old);
     pu.v[e] = pu_new;
     qp.v[e] = qp_new;
     qn.v[e] = qn_new;
   }
   store_row(pu, a.U + u * kp, lane, kp);
-  store_row(qp, a.I + p * kp, lane, kp);
+  if (!same) store_row(qp, a.I + p * kp, lane, kp);
   store_row(qn, a.I + n * kp, lane, kp);
   return true;
 }
@@ -128,24 +144,29 @@ __device__ __forceinline__ int64_t draw_negative_t(const A& a, const int32_t* it
 // and q_p are loaded once and carried through the steps, as one thread of the reference
 // sees its own writes (BPREngine::update :178-220 per step); the negatives are drawn first
 // and their rows loaded together (a repeated negative takes the updated row of its earlier
-// draw).  Each row is stored after its last update.
+// draw).  Each row's net change is added to memory after its last update (add_row).
 template <typename T, int E>
 __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int64_t p,
                                              const int64_t (&n)[4], int nn, int lane) {
   const int kp = a.kp;
-  Row<T, E> pu, qp, qn[4];
-  load_row(pu, a.U + u * kp, lane, kp);
-  load_row(qp, a.I + p * kp, lane, kp);
+  Row<T, E> pu, qp, qn[4], pu0, qp0, qn0[4];
+  load_row(pu0, a.U + u * kp, lane, kp);
+  load_row(qp0, a.I + p * kp, lane, kp);
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (j < nn) load_row(qn[j], a.I + n[j] * kp, lane, kp);
-  T bp = T(0), bn[4] = {T(0), T(0), T(0), T(0)};
+    if (j < nn) load_row(qn0[j], a.I + n[j] * kp, lane, kp);
+  pu = pu0;
+  qp = qp0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) qn[j] = qn0[j];
+  T bp0 = T(0), bn0[4] = {T(0), T(0), T(0), T(0)};
   if (a.use_biases) {
-    bp = ld_shared(a.bias + p);
+    bp0 = ld_shared(a.bias + p);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (j < nn) bn[j] = ld_shared(a.bias + n[j]);
+      if (j < nn) bn0[j] = ld_shared(a.bias + n[j]);
   }
+  T bp = bp0, bn[4] = {bn0[0], bn0[1], bn0[2], bn0[3]};
   bool ok = true;
   const T lr = a.lr;
 #pragma unroll
@@ -156,7 +177,9 @@ __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int
     for (int i = 0; i < j; ++i)
       if (n[i] == n[j]) {
         qn[j] = qn[i];
+        qn0[j] = qn0[i];
         bn[j] = bn[i];
+        bn0[j] = bn0[i];
       }
     T part = T(0);
 #pragma unroll
@@ -190,13 +213,13 @@ __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int
     for (int i = j + 1; i < 4; ++i)
       if (i < nn && n[i] == n[j]) last = false;
     if (last) {
-      store_row(qn[j], a.I + n[j] * kp, lane, kp);
-      if (a.use_biases && lane == 0) st_shared(a.bias + n[j], bn[j]);
+      add_row(qn[j], qn0[j], a.I + n[j] * kp, lane, kp);
+      if (a.use_biases && lane == 0) unsafeAtomicAdd(a.bias + n[j], bn[j] - bn0[j]);
     }
   }
-  store_row(pu, a.U + u * kp, lane, kp);
-  store_row(qp, a.I + p * kp, lane, kp);
-  if (a.use_biases && lane == 0) st_shared(a.bias + p, bp);
+  add_row(pu, pu0, a.U + u * kp, lane, kp);
+  add_row(qp, qp0, a.I + p * kp, lane, kp);
+  if (a.use_biases && lane == 0) unsafeAtomicAdd(a.bias + p, bp - bp0);
   return ok;
 }
 

@@ -1110,10 +1110,11 @@ static BprArgs<T> bpr_args(qmfx_ctx* c, double lr, double bl, double ul, double 
   a.use_biases = ub;
   a.kp = c->kp;
   a.bad = c->bad;
-  // Hogwild width: concurrent waves collide when they touch the same user or item row, and
-  // a collision drops an update.  Keep the expected number of concurrent waves per row
-  // small: ≈ min(nusers, nitems)/16 waves, capped at 16 waves per CU (4096), at least 1
-  // (a 3-user problem runs serially, as the reference's 1-thread default does).
+  // Hogwild width: concurrent waves that touch the same user or item row read it stale (row
+  // changes are added atomically, so no update is lost).  Keep the expected number of
+  // concurrent waves per row small: ≈ min(nusers, nitems)/16 waves, capped at 16 waves per
+  // CU (4096), at least 1 (a 3-user problem runs serially, as the reference's 1-thread
+  // default does).
   const int64_t rows = std::min(c->s[0].n, c->s[1].n);
   a.waves = (int)std::max<int64_t>(1, std::min<int64_t>({4096, rows / 16, std::max<int64_t>(c->npos, 1)}));
   return a;

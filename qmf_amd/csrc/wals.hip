@@ -577,7 +577,9 @@ void wals_direct_kernel(SolveArgs<T> a) {
     double xb = 0.0, xx = 0.0;
     for (int j = lane; j < KP; j += 64) {
       const T xj = S.xs[j];
-      a.X[row * KP + (Perm<NT>::template split<T> ? Perm<NT>::phys(j) : j)] = xj;
+      // a failed row stores x = 0 (loss term 0), like the whitened kernel; the caller
+      // re-solves it
+      a.X[row * KP + (Perm<NT>::template split<T> ? Perm<NT>::phys(j) : j)] = bad ? T(0) : xj;
       xb += (double)xj * (double)borig[j];
       xx += (double)xj * (double)xj;
     }

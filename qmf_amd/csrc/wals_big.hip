@@ -60,6 +60,7 @@ struct BigShared {
   T invd[C::KP];
   T part[C::NW * 16];
   double red[C::NW];
+  int bad;  // wave 0's pivot flag, for every wave's output stores
 };
 
 // Panel p of the right-looking Cholesky, by ONE wave: rows 16p..KP-1 of column block p are
@@ -389,6 +390,9 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     __syncthreads();
   }
 
+  if (tid == 0) S.bad = bad;
+  __syncthreads();
+
   // ---- backward solve Lᵀ x = y ----------------------------------------------------------
   for (int I = NT - 1; I >= 0 && !(a.ablate & 8); --I) {
     T part = T(0);
@@ -423,7 +427,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   // ---- output: x, row loss = Σc − xᵀb − λ‖x‖² ----------------------------------------------
   double xb = 0.0, xx = 0.0;
   if (tid < KP) {
-    const T xi = S.xs[tid];
+    const T xi = S.bad ? T(0) : S.xs[tid];  // a failed row stores x = 0 (re-solved by the caller)
     a.X[row * KP + tid] = xi;
     xb = (double)xi * (double)S.borig[tid];
     xx = (double)xi * (double)xi;

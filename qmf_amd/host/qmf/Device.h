@@ -12,12 +12,14 @@
 namespace qmf {
 
 // Which GPU and which arithmetic the engines use.  Defaults come from the environment
-// (QMF_DEVICE, QMF_PRECISION), then device 0 and fp32; the CLIs expose --device and
-// --precision.  fp64 matches the reference's Double arithmetic to ~1e-12; fp32 meets the
-// 1e-4 factor tolerance on well-conditioned systems at twice the throughput.
+// (QMF_DEVICE, QMF_PRECISION), then device 0 and fp64 (the reference's `Double`,
+// Types.h:24); the CLIs expose --device and --precision.  fp64 matches the reference's
+// arithmetic to ~1e-12.  fp32 (opt-in) stores the factors in fp32: on well-posed problems it
+// meets the 1e-4 factor tolerance at the reference's λ/α, but its error grows as cond·6e-8,
+// so rank-deficient inputs (e.g. more factors than distinct fixed-side rows) need fp64.
 struct DeviceOptions {
   int device = envInt("QMF_DEVICE", 0);
-  int precision = envInt("QMF_PRECISION", 32);
+  int precision = envInt("QMF_PRECISION", 64);
 
   static int envInt(const char* name, int def) {
     const char* v = std::getenv(name);

@@ -29,8 +29,8 @@ DEFINE_uint64(eval_num_neg, 3, "number of negatives generated per positive in ev
 DEFINE_int32(eval_seed, 42, "random seed for generating evaluation set and test users");
 DEFINE_uint64(nthreads, 16, "number of host threads (evaluation, output)");
 DEFINE_int32(device, qmf::DeviceOptions::envInt("QMF_DEVICE", 0), "GPU ordinal");
-DEFINE_int32(precision, qmf::DeviceOptions::envInt("QMF_PRECISION", 32),
-             "device arithmetic: 32 (fp32) or 64 (fp64)");
+DEFINE_int32(precision, qmf::DeviceOptions::envInt("QMF_PRECISION", 64),
+             "device arithmetic: 64 (fp64, the reference's Double; default) or 32 (fp32)");
 DEFINE_uint64(seed, 0, "seed of the factor init and SGD sampling (0 = random_device)");
 // datasets
 DEFINE_string(train_dataset, "", "filename of training dataset");

@@ -19,8 +19,8 @@ DEFINE_string(distribution_file, "", "uniform distribution file, for repeatable 
 // settings
 DEFINE_int32(nthreads, 16, "number of host threads (ingest, evaluation, output)");
 DEFINE_int32(device, qmf::DeviceOptions::envInt("QMF_DEVICE", 0), "GPU ordinal");
-DEFINE_int32(precision, qmf::DeviceOptions::envInt("QMF_PRECISION", 32),
-             "device arithmetic: 32 (fp32) or 64 (fp64)");
+DEFINE_int32(precision, qmf::DeviceOptions::envInt("QMF_PRECISION", 64),
+             "device arithmetic: 64 (fp64, the reference's Double; default) or 32 (fp32)");
 // datasets
 DEFINE_string(train_dataset, "", "filename of training dataset");
 DEFINE_string(test_dataset, "", "filename of test dataset");

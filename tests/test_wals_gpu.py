@@ -1,10 +1,13 @@
 """WALS parity on the MI355X: the HIP path (through the C ABI) against the CPU oracle on
-identical inputs and initial factors.
+identical inputs and initial factors, at the reference's λ = 0.05, α = 40.
 
 Tolerances (BASELINE.json north_star: factors within 1e-4 relative; index/ID bookkeeping
-bit-exact): fp64 path 1e-9 normwise-relative per half step (only rounding differs: MFMA
-accumulation order and Cholesky vs Bunch-Kaufman), fp32 path 1e-4.
+bit-exact): fp64 path (the CLI default) 1e-9 normwise-relative per half step (only rounding
+differs: MFMA accumulation order and Cholesky vs Bunch-Kaufman); fp32 path 1e-4 on
+well-posed inputs, and its k·cond·u bound on an ill-conditioned one.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -15,6 +18,7 @@ from helpers import csr_from_triples, load_ml100k, load_tiny, rel_err, synth
 pytestmark = pytest.mark.gpu
 
 LAM, ALPHA = 0.05, 40.0
+NTHR = min(16, len(os.sched_getaffinity(0)))  # oracle threads (the box's CPU share)
 
 
 def make_pair(users, items, values, k, precision, init=None, seed=0, lam=LAM, alpha=ALPHA):
@@ -51,28 +55,59 @@ def test_mfma_layout_f32_f64():
         np.testing.assert_array_equal(qmf_amd.selftest_mfma(prec, A, B), A @ B)
 
 
-@pytest.mark.parametrize("precision,tol,lam", [(64, 1e-9, LAM), (32, 1e-4, 5.0)])
 @pytest.mark.parametrize("k", [8, 16, 30])
-def test_tiny_half_steps(precision, tol, lam, k):
-    # The tiny fixture has 9 users: with λ = 0.05 its item systems have cond ≈ 1e4–1e5,
-    # beyond what fp32 factors can resolve to 1e-4 (fp32 error ≈ cond·6e-8).  fp64 is
-    # checked at the reference λ; fp32 at a well-conditioned λ.
+def test_tiny_half_steps(k):
+    """The edge-case fixture (duplicates, zero values, signed ids) through the default fp64
+    path at the reference's λ/α, per half in lock-step."""
     u, i, v = load_tiny()
-    o, c = make_pair(u, i, v, k, precision, seed=k, lam=lam)
+    o, c = make_pair(u, i, v, k, 64, seed=k)
     for epoch in range(2):
         for side in (0, 1):
             lo = o.iterate(side)
-            ld = c.wals_half(side, ALPHA, lam) / (o.nusers * o.nitems)
-            assert rel_err(c.factors(side), o.factors(side)) < tol
-            assert abs(ld - lo) <= tol * max(1.0, abs(lo)) * 10
+            ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+            assert rel_err(c.factors(side), o.factors(side)) < 1e-9
+            assert abs(ld - lo) <= 1e-8 * max(1.0, abs(lo))
             # keep the two in lock-step for the next half
             c.set_factors(side, o.factors(side))
+
+
+def row_conditions(o, side):
+    """cond₂ of every row system A = YᵀY + Σ αv y yᵀ + λI of `side` (numpy, from the
+    oracle's CSR and fixed-side factors)."""
+    rp, col, val = o.csr(side)
+    Y = o.factors(1 - side)
+    M = Y.T @ Y + LAM * np.eye(Y.shape[1])
+    out = []
+    for r in range(len(rp) - 1):
+        y = Y[col[rp[r]:rp[r + 1]]]
+        out.append(np.linalg.cond(M + (y.T * (ALPHA * val[rp[r]:rp[r + 1]])) @ y))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_fp32_error_is_bounded_by_conditioning(k):
+    """The opt-in fp32 path on an ILL-conditioned fixture at the reference's λ/α: the tiny
+    fixture has 9 users, so its item systems reach cond ≈ 1e4–1e5 and no fp32 solve (nor
+    fp32 storage of the fixed side alone) can be within 1e-4 of the fp64 reference there.
+    What fp32 does guarantee is the normwise bound k·cond·u (u = 2⁻²⁴); that is checked
+    here.  Well-posed inputs meet 1e-4 (the tests below and
+    tests/test_configs_gpu.py)."""
+    u, i, v = load_tiny()
+    o, c = make_pair(u, i, v, k, 32, seed=k)
+    for side in (0, 1):
+        kappa = row_conditions(o, side).max()
+        o.iterate(side)
+        c.wals_half(side, ALPHA, LAM)
+        err = rel_err(c.factors(side), o.factors(side))
+        assert err < k * kappa * 2.0 ** -24, (side, err, kappa)
+        c.set_factors(side, o.factors(side))
 
 
 @pytest.mark.parametrize("precision,tol", [(64, 1e-9), (32, 1e-4)])
 def test_ml100k_shape_ten_epochs(precision, tol):
     """The survey's reference-pinned dataset: 10 epochs run
-    independently on both sides; factors and the per-epoch loss must track the oracle."""
+    independently on both sides at the reference's λ/α; factors and the per-epoch loss must
+    track the oracle (fp32 measured at ≈1e-5 after 10 epochs)."""
     d = load_ml100k()
     k = 30
     init = d["init"][: 1682 * k].reshape(1682, k)
@@ -82,11 +117,12 @@ def test_ml100k_shape_ten_epochs(precision, tol):
     for _ in range(10):
         c.wals_half(0, ALPHA, LAM)
         dl.append(c.wals_half(1, ALPHA, LAM) / (o.nusers * o.nitems))
-    assert abs(dl[0] - float(d["ref_loss_epoch1"])) < 5e-6 * (1 if precision == 64 else 10)
-    assert abs(dl[9] - float(d["ref_loss_epoch10"])) < 5e-7 * (1 if precision == 64 else 100)
-    np.testing.assert_allclose(dl, ol, rtol=tol * 10)
-    assert rel_err(c.factors(0), o.factors(0)) < tol * 10
-    assert rel_err(c.factors(1), o.factors(1)) < tol * 10
+    # the reference's printed losses carry 6 significant digits
+    assert abs(dl[0] - float(d["ref_loss_epoch1"])) < 5e-6
+    assert abs(dl[9] - float(d["ref_loss_epoch10"])) < 5e-7
+    np.testing.assert_allclose(dl, ol, rtol=tol)
+    assert rel_err(c.factors(0), o.factors(0)) < tol
+    assert rel_err(c.factors(1), o.factors(1)) < tol
 
 
 @pytest.mark.parametrize("k", [32, 64, 96, 128])
@@ -145,6 +181,8 @@ def test_indefinite_rows_are_flagged():
     o, c = make_pair(u, i, v, 8, 64, init=np.full((3, 8), 0.3), lam=0.01, alpha=40.0)
     c.wals_half(0, 40.0, 0.01)
     assert 0 in set(c.failed_rows().tolist())
+    # a flagged row is written as x = 0 (never NaN) for the caller's re-solve
+    assert np.array_equal(c.factors(0)[0], np.zeros(8))
 
 
 @pytest.mark.parametrize("k,precision", [(256, 32), (128, 32), (64, 32), (64, 64), (32, 64)])
@@ -173,38 +211,31 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, monkeypatch):
                                          (200, 64)])
 def test_large_k_multiwave_rows(k, precision):
     """k beyond one wave's registers (fp32 > 128, fp64 > 64): the multi-wave row kernel
-    (LDS-staged Gram, distributed Cholesky) and the strip YᵀY, against the oracle; rows
-    from 1 to ~150 signals cover partial LDS stages and every panel-slot count."""
-    u, i, v = synth(1500, 300, 40000, seed=k)
-    # fp32 error ≈ cond·6e-8: at k = 256 these item systems have cond ≈ 2e4 at λ = 5, where
-    # a float32 LAPACK solve of the same systems is itself off by 2.5e-4 (this kernel: 1.4e-4).
-    # fp32 is therefore checked at a well-conditioned λ; fp64 (the logic check, 1e-9) at the
-    # reference λ.
-    lam = 0.05 if precision == 64 else 50.0
-    o, c = make_pair(u, i, v, k, precision, seed=3, lam=lam)
+    (LDS-staged Gram, distributed Cholesky) and the strip YᵀY, against the oracle at the
+    reference's λ/α; rows from 1 to ~150 signals cover partial LDS stages and every
+    panel-slot count.  800 items ≫ k keeps the item systems well-posed for fp32."""
+    u, i, v = synth(4000, 800, 100000, seed=k)
+    o, c = make_pair(u, i, v, k, precision, seed=3)
     tol = 1e-9 if precision == 64 else 1e-4
     for side in (0, 1):
-        lo = o.iterate(side)
-        ld = c.wals_half(side, ALPHA, lam) / (o.nusers * o.nitems)
+        lo = o.iterate(side, NTHR)
+        ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
         assert rel_err(c.factors(side), o.factors(side)) < tol, side
-        assert abs(ld - lo) < tol * abs(lo) * 10
+        assert abs(ld - lo) < tol * abs(lo), side
         c.set_factors(side, o.factors(side))  # lock-step: each half checked on its own
 
 
 @pytest.mark.parametrize("k", [96, 128])
 def test_long_rows_fp32_direct(k):
-    """Rows with hundreds of signals on the fp32 direct kernel: the LDS-staged (column,
-    value) chunks of the split-bf16 Gram (prologue, chunk hand-over, ragged last step, zero-row
-    padding) against the oracle, on both halves."""
-    u, i, v = synth(12000, 60, 30000, seed=k)  # ~500 signals per item, ~2.5 per user
-    # fp32 error ≈ cond·6e-8: at α = 40 these 500-signal item systems have cond ≈ 3e4 (the
-    # fp64 path is 3e-12 off there, fp32 2e-3, on the split and the f32-MFMA Gram alike), so
-    # fp32 is checked on well-conditioned ones (α = 1, λ = 5: ≈2e-6)
-    lam, alpha = 5.0, 1.0
-    o, c = make_pair(u, i, v, k, 32, seed=4, lam=lam, alpha=alpha)
+    """Rows with hundreds of signals on the fp32 direct kernel at the reference's λ/α: the
+    LDS-staged (column, value) chunks of the split-bf16 Gram (prologue, chunk hand-over,
+    ragged last step, zero-row padding) against the oracle, on both halves.  ~500 signals
+    per item, ~5 per user, 400 items ≫ k."""
+    u, i, v = synth(40000, 400, 200000, seed=k)
+    o, c = make_pair(u, i, v, k, 32, seed=4)
     for side in (0, 1):
-        lo = o.iterate(side)
-        ld = c.wals_half(side, alpha, lam) / (o.nusers * o.nitems)
+        lo = o.iterate(side, NTHR)
+        ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
         assert rel_err(c.factors(side), o.factors(side)) < 1e-4, side
         assert abs(ld - lo) < 1e-4 * abs(lo), side
         c.set_factors(side, o.factors(side))
