@@ -42,20 +42,57 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
-    """Reference-structure CPU port (oracle/qmf_oracle.cpp: hash lookup per nnz, per-row
-    k×k copies, full k×k Gram, Bunch-Kaufman dsysv restatement, serial YᵀY) timed on a
-    bounded sample of the SAME matrix and extrapolated to one epoch."""
+MKL = "/opt/conda/lib/libmkl_rt.so.1"
+
+
+def cpu_share():
+    """Threads for the CPU baseline: `nproc` (which honours OMP_NUM_THREADS, as the box sets
+    it to its CPU share), bounded by the affinity mask and the cgroup CPU quota."""
+    import subprocess
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except Exception:
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except Exception:
+        nproc = aff
+    n = min(x for x in (nproc, aff, quota) if x)
+    return n, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def oracle_lib():
+    """The oracle with the host LAPACK's dsysv_ when the image has one (MKL, sequential: the
+    survey's reference build, BASELINE.md CPU-baseline plan), else the restated netlib
+    dsytf2/dsytrs.  Returns (pyoracle module, LAPACK description)."""
+    if os.path.exists(MKL) and "ORC_LAPACK" not in os.environ:
+        os.environ["ORC_LAPACK"] = MKL
+        os.environ["MKL_THREADING_LAYER"] = "SEQUENTIAL"
+        os.environ["MKL_NUM_THREADS"] = "1"
+    os.environ["OMP_NUM_THREADS"] = "1"
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
+    lap = os.environ.get("ORC_LAPACK")
+    return po, ("dsysv_ from %s (sequential)" % lap) if lap else \
+        "restated netlib dsytf2+dsytrs (no host LAPACK)"
 
+
+def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
+    """Reference-structure CPU port (oracle/qmf_oracle.cpp: hash lookup per nnz, per-row
+    k×k copies, full k×k Gram, dsysv, serial YᵀY) timed on a bounded sample of the SAME
+    matrix: strided rows of each half and YᵀY over a row subset, scaled to one epoch."""
+    po, lapack = oracle_lib()
     nu, ni, _, k, _ = cfg
     urp, ucol, uval = ctx.download_csr(0)
     irp, icol, ival = ctx.download_csr(1)
     U = ctx.factors(0)
     I = ctx.factors(1)
     total = 0.0
-    detail = {}
+    detail = {"lapack": lapack}
     for side in (0, 1):
         rp, col, val = (urp, ucol, uval) if side == 0 else (irp, icol, ival)
         Y = I if side == 0 else U
@@ -90,6 +127,64 @@ def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
                                        t_yty=t_yty, t_rows=t_rows)
         total += yty_full + rows_full
     return total, detail
+
+
+def cpu_epoch(ctx, cfg, nthreads):
+    """One FULL epoch of the reference-structure port (both halves, serial YᵀY, every row)
+    on this matrix from the device's current item factors.  Minutes at C3: opt-in
+    (--cpu-baseline epoch)."""
+    po, lapack = oracle_lib()
+    nu, ni, _, k, _ = cfg
+    t0 = time.perf_counter()
+    urp, ucol, uval = ctx.download_csr(0)
+    irp, icol, ival = ctx.download_csr(1)
+    o = po.OracleWALS.from_csr(nu, ni, urp, ucol, uval, irp, icol, ival, k, LAM, ALPHA)
+    del urp, ucol, uval, irp, icol, ival
+    o.set_factors(1, ctx.factors(1))
+    t_build = time.perf_counter() - t0
+    log("cpu epoch: oracle built in %.1fs; running one epoch on %d threads" % (t_build, nthreads))
+    t1 = time.perf_counter()
+    o.iterate(0, nthreads)
+    t_u = time.perf_counter() - t1
+    log("cpu epoch: user half %.1fs" % t_u)
+    loss = o.iterate(1, nthreads)
+    t = time.perf_counter() - t1
+    return t, {"lapack": lapack, "t_user_half": round(t_u, 3), "t_item_half": round(t - t_u, 3),
+               "t_build": round(t_build, 3), "loss": loss}
+
+
+def parity_check(ctx, cfg, nthreads, nsample=1000):
+    """Full-size parity: one more (untimed) epoch; `nsample` rows of each half are re-solved
+    by the oracle's updateFactorsForOne (WALSEngine.cpp:266-310) against the fixed side the
+    device used (its own values), and compared with the device's rows and row losses."""
+    po, _ = oracle_lib()
+    nu, ni, _, k, seed = cfg
+    rng = np.random.default_rng(seed + 7)
+    I_prev = ctx.factors(1)
+    ctx.wals_half(0, ALPHA, LAM)
+    U, lu = ctx.factors(0), ctx.row_losses(0)
+    ctx.wals_half(1, ALPHA, LAM)
+    I, li = ctx.factors(1), ctx.row_losses(1)
+    out = {"rows_per_half": nsample}
+    worst = 0.0
+    for side, Y, X, rl in ((0, I_prev, U, lu), (1, U, I, li)):
+        rp, col, val = ctx.download_csr(side)
+        rows = np.sort(rng.choice(len(rp) - 1, nsample, replace=False))
+        t0 = time.perf_counter()
+        x, loss = po.solve_rows(Y, rp, col, val, rows, ALPHA, LAM, nthreads)
+        dev = X[rows]
+        row_err = np.linalg.norm(dev - x, axis=1) / np.maximum(np.linalg.norm(x, axis=1), 1e-300)
+        rel = float(np.linalg.norm(dev - x) / np.linalg.norm(x))
+        lrel = float(np.max(np.abs(rl[rows] - loss) / np.maximum(np.abs(loss), 1e-300)))
+        out["side%d" % side] = {"max_row_rel_err": float(row_err.max()), "normwise_rel_err": rel,
+                                "max_row_loss_rel_err": lrel,
+                                "oracle_s": round(time.perf_counter() - t0, 2)}
+        worst = max(worst, float(row_err.max()))
+        del rp, col, val
+    out["max_rel_err"] = worst
+    out["tolerance"] = 1e-4
+    out["pass"] = bool(worst <= 1e-4)
+    return out
 
 
 # kernels of each timed class (names as rocprofv3 reports them)
@@ -159,6 +254,7 @@ def bench_bpr(args, rank, world):
     trip = eval_triplets(urp, ucol, ni, num_neg, seed)
     del users, perm
     ctx.sync()
+    log("c4: data ready (%d positives, %d eval triplets)" % (nnz, len(trip)))
 
     def step(e):
         ctx.bpr_epoch(seed * 1000 + e, num_neg, lr * 0.9 ** e, *lam, False, shuffle=e > 0)
@@ -174,6 +270,7 @@ def bench_bpr(args, rank, world):
         loss = step(args.warmup + e)
     ctx.sync()
     el = time.perf_counter() - t1
+    log("c4: %d timed epochs in %.3fs" % (args.steps, el))
     st = ctx.solve_stats()
     upd = nnz * num_neg * args.steps
     sec = st["ms"] / 1e3 / max(st["launches"], 1)
@@ -193,20 +290,26 @@ def bench_bpr(args, rank, world):
                      "launch_ms": round(sec * 1e3, 3)},
         "eval_loss": loss,
     }
-    if not args.no_cpu_baseline and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle as po
+    if args.cpu_baseline != "none" and rank == 0:
+        # one full reference-structure Hogwild epoch (BPREngine::optimize with
+        # numHogwildThreads = nthreads) + its evaluation pass, from the device's factors
+        po, _ = oracle_lib()
+        nthreads, host = cpu_share()
+        log("c4: CPU baseline (one Hogwild epoch, %d threads)" % nthreads)
         U, I = ctx.factors(0), ctx.factors(1)
         b = np.zeros(ni)
-        sample = trip[np.random.default_rng(1).choice(len(trip), 3_000_000, replace=False)]
-        t0 = time.perf_counter()
-        po.bpr_update_seq(U, I, b, sample, lr, *lam, False)
-        t = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(len(sample) / t, 1), "unit": "updates/s", "cores": 1,
-                               "kind": "port",
-                               "sample": "oracle BPREngine::update, serial, on 3M of this "
-                                         "workload's triplets (%.1f s); the reference's "
-                                         "Hogwild default is 1 thread" % t}
+        users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(urp))
+        perm = np.random.default_rng(seed).permutation(nnz)
+        t_up, t_ev, closs = po.bpr_hogwild_epoch(U, I, b, users[perm], ucol[perm], ni, num_neg,
+                                                 nthreads, seed, lr, *lam, False, trip)
+        t = t_up + t_ev
+        out["cpu_baseline"] = {"value": round(nnz * num_neg / t, 1), "unit": "updates/s",
+                               "cores": nthreads, "kind": "port", "ms_per_epoch": round(t * 1e3, 1),
+                               "sample": "one full Hogwild epoch (%d threads, %d updates) + the "
+                                         "evaluation pass of the reference-structure port on "
+                                         "this workload: %.1f s + %.1f s" % (nthreads, nnz * num_neg,
+                                                                             t_up, t_ev),
+                               "detail": {"host": host, "eval_loss": closs / len(trip)}}
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -219,8 +322,12 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline", default="sample", choices=("sample", "epoch", "none"))
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
+    if args.no_cpu_baseline:
+        args.cpu_baseline = "none"
 
     import qmf_amd
 
@@ -328,20 +435,25 @@ def main():
         "hbm_roofline_frac_epoch": round(hbm_frac_epoch, 4),
         "loss": loss / nu / ni,
     }
-    if not args.no_cpu_baseline and world == 1:
-        cores = os.cpu_count() or 1
-        try:
-            affinity = len(os.sched_getaffinity(0))
-        except Exception:
-            affinity = cores
-        nthreads = max(1, min(affinity, 16))
-        tcpu, detail = cpu_baseline(ctx, CONFIGS[args.config], nthreads, args.cpu_budget)
+    nthreads, host = cpu_share()
+    if not args.no_parity and world == 1:
+        t0 = time.perf_counter()
+        out["parity"] = parity_check(ctx, CONFIGS[args.config], nthreads)
+        log("parity check %.1fs: %s" % (time.perf_counter() - t0, out["parity"]))
+    if args.cpu_baseline != "none" and world == 1:
+        if args.cpu_baseline == "epoch":
+            tcpu, detail = cpu_epoch(ctx, CONFIGS[args.config], nthreads)
+            sample = ("one full epoch (user half + item half, every row, serial YtY) of the "
+                      "reference-structure port on this matrix: %.1f s" % tcpu)
+        else:
+            tcpu, detail = cpu_baseline(ctx, CONFIGS[args.config], nthreads, args.cpu_budget)
+            sample = ("strided row samples of each half of this matrix and YtY on a row "
+                      "subset, scaled to one epoch = %.1f s (a full epoch: --cpu-baseline "
+                      "epoch)" % tcpu)
+        detail["host"] = host
         out["cpu_baseline"] = {"value": round((nu + ni) / tcpu, 1), "unit": "solves/s",
-                               "cores": nthreads, "kind": "port",
-                               "sample": "oracle (reference-structure C++ port) on strided row "
-                                         "samples of this matrix, YtY timed on a row subset, "
-                                         "extrapolated to one epoch = %.1f s" % tcpu,
-                               "detail": detail}
+                               "cores": nthreads, "kind": "port", "ms_per_epoch": round(tcpu * 1e3, 1),
+                               "sample": sample, "detail": detail}
     print(json.dumps(out), flush=True)
 
 

@@ -57,6 +57,10 @@ def lib():
         L.orc_xtx.argtypes = [c_f64p, ctypes.c_int64, ctypes.c_int, c_f64p]
         L.orc_linear_symmetric_solve.restype = ctypes.c_int
         L.orc_linear_symmetric_solve.argtypes = [c_f64p, c_f64p, ctypes.c_int]
+        L.orc_solve_rows.restype = ctypes.c_int
+        L.orc_solve_rows.argtypes = [c_f64p, ctypes.c_int64, ctypes.c_int, c_i64p, c_i32p, c_f32p,
+                                     c_i64p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_int, c_f64p, c_f64p]
         L.orc_update_one.restype = ctypes.c_double
         L.orc_update_one.argtypes = [c_f64p, ctypes.c_int64, ctypes.c_int, c_i64p, c_f64p,
                                      ctypes.c_int64, c_f64p, ctypes.c_double, ctypes.c_double,
@@ -72,6 +76,13 @@ def lib():
         L.orc_bpr_loss_sum.restype = ctypes.c_double
         L.orc_bpr_loss_sum.argtypes = [c_f64p, c_f64p, c_f64p, ctypes.c_int, c_i64p,
                                        ctypes.c_int64, ctypes.c_int]
+        L.orc_bpr_hogwild_epoch.restype = ctypes.c_int
+        L.orc_bpr_hogwild_epoch.argtypes = [c_f64p, c_f64p, c_f64p, ctypes.c_int, c_i64p, c_i64p,
+                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                            ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                            ctypes.c_double, ctypes.c_int, c_i64p, ctypes.c_int64,
+                                            c_f64p, c_f64p, c_f64p]
         L.orc_bpr_sets.restype = ctypes.c_int
         L.orc_bpr_sets.argtypes = [c_i64p, c_i64p, c_f64p, ctypes.c_int64, c_i64p, c_i64p,
                                    c_f64p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
@@ -209,6 +220,25 @@ def update_one(Y, cols, vals, YtY, alpha, lam):
     return x, loss
 
 
+def solve_rows(Y, rowptr, col, val, rows, alpha, lam, nthreads=1):
+    """updateFactorsForOne (WALSEngine.cpp:266-310) for the given rows of a CSR whose column
+    indices index Y directly; YtY over all of Y.  Returns (x [len(rows)×k], row losses)."""
+    Y = np.ascontiguousarray(Y, np.float64)
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    val = np.ascontiguousarray(val, np.float32)
+    rows = np.ascontiguousarray(rows, np.int64)
+    k = Y.shape[1]
+    x = np.empty((len(rows), k), np.float64)
+    loss = np.empty(len(rows), np.float64)
+    info = lib().orc_solve_rows(_p(Y, c_f64p), Y.shape[0], k, _p(rowptr, c_i64p), _p(col, c_i32p),
+                                _p(val, c_f32p), _p(rows, c_i64p), len(rows), float(alpha),
+                                float(lam), int(nthreads), _p(x, c_f64p), _p(loss, c_f64p))
+    if info != 0:
+        raise RuntimeError("dsysv info=%d" % info)
+    return x, loss
+
+
 def bpr_update_seq(U, I, bias, triplets, lr, bias_lambda, user_lambda, item_lambda, use_biases):
     """In-place BPREngine::update over triplets (BPREngine.cpp:178-220)."""
     for a in (U, I, bias):
@@ -233,6 +263,27 @@ def bpr_loss_sum(U, I, bias, triplets, use_biases):
     t = np.ascontiguousarray(triplets, np.int64)
     return lib().orc_bpr_loss_sum(_p(U, c_f64p), _p(I, c_f64p), _p(bias, c_f64p), U.shape[1],
                                   _p(t, c_i64p), len(t), int(use_biases))
+
+
+def bpr_hogwild_epoch(U, I, bias, pos_user, pos_item, nitems, num_neg, nthreads, seed, lr,
+                      bias_lambda, user_lambda, item_lambda, use_biases, eval_set):
+    """One reference-structure Hogwild BPR epoch + evaluation (CPU BASELINE ONLY; see
+    orc_bpr_hogwild_epoch).  U/I/bias updated in place.  Returns (t_update, t_eval, loss)."""
+    for a in (U, I, bias):
+        assert a.dtype == np.float64 and a.flags.c_contiguous
+    pu = np.ascontiguousarray(pos_user, np.int64)
+    pi = np.ascontiguousarray(pos_item, np.int64)
+    ev = np.ascontiguousarray(eval_set, np.int64)
+    out = np.zeros(3, np.float64)
+    rc = lib().orc_bpr_hogwild_epoch(_p(U, c_f64p), _p(I, c_f64p), _p(bias, c_f64p), U.shape[1],
+                                     _p(pu, c_i64p), _p(pi, c_i64p), len(pu), U.shape[0],
+                                     int(nitems), int(num_neg), int(nthreads), int(seed),
+                                     lr, bias_lambda, user_lambda, item_lambda, int(use_biases),
+                                     _p(ev, c_i64p), len(ev), _p(out[0:], c_f64p),
+                                     _p(out[1:], c_f64p), _p(out[2:], c_f64p))
+    if rc:
+        raise RuntimeError("gradients too big")
+    return float(out[0]), float(out[1]), float(out[2])
 
 
 def bpr_sets(users, items, values, test=None, eval_num_neg=3, eval_seed=42):

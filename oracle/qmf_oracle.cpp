@@ -24,6 +24,7 @@
 //  what dsysv_ runs when lwork = n is below the blocked-path workspace (Matrix.cpp:81-96).
 // =====================================================================================
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -307,9 +308,16 @@ static void computeXtX(const std::vector<double>& X, size_t nrows, int k, std::v
   }
 }
 
+// Index whose ids are the idx themselves (synthetic CSRs, where id = row/column index):
+// the same lookups as IdIndex without building a hash over 10^7 ids for a row-sample check.
+struct IdentityIndex {
+  size_t idx(int64_t id) const { return (size_t)id; }
+};
+
 // WALSEngine::updateFactorsForOne (Matrix& overload, WALSEngine.cpp:266-310)
-static double updateFactorsForOne(std::vector<double>& X, const IdIndex& leftIndex,
-                                  const std::vector<double>& Y, const IdIndex& rightIndex,
+template <class LIndex, class RIndex>
+static double updateFactorsForOne(std::vector<double>& X, const LIndex& leftIndex,
+                                  const std::vector<double>& Y, const RIndex& rightIndex,
                                   const SignalGroup& sg, std::vector<double> A /*YtY by value*/,
                                   double alpha, double lambda, int n, int* info_out) {
   double loss = 0.0;
@@ -586,6 +594,56 @@ double orc_update_one(const double* Y, int64_t nY, int k, const int64_t* cols,
   return loss;
 }
 
+// Parity checker at full size: re-solves `nrows` rows of a CSR (ids = indices) with
+// updateFactorsForOne against the given fixed side Y (nY×k, the device's own values), with
+// YtY = computeXtX(Y) summed over `nthreads` row blocks (fixed order; the serial sum differs
+// only by rounding).  Writes x (nrows×k) and the row losses.  Returns the first nonzero
+// dsysv info, or 0.
+int orc_solve_rows(const double* Y, int64_t nY, int k, const int64_t* rowptr,
+                   const int32_t* col, const float* val, const int64_t* rows, int64_t nrows,
+                   double alpha, double lambda, int nthreads, double* x_out, double* loss_out) {
+  if (nthreads < 1) nthreads = 1;
+  std::vector<double> y(Y, Y + (size_t)nY * k);
+  std::vector<std::vector<double>> part((size_t)nthreads);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([&, t]() {
+        const int64_t b = nY * t / nthreads, e = nY * (t + 1) / nthreads;
+        std::vector<double> sub(y.begin() + b * k, y.begin() + e * k);
+        computeXtX(sub, (size_t)(e - b), k, part[(size_t)t]);
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<double> YtY((size_t)k * k, 0.0);
+  for (int t = 0; t < nthreads; ++t)
+    for (size_t i = 0; i < YtY.size(); ++i) YtY[i] += part[(size_t)t][i];
+  const IdentityIndex ident;
+  std::vector<int> infos((size_t)nthreads, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([&, t]() {
+      std::vector<double> X((size_t)k, 0.0);
+      struct One {
+        size_t idx(int64_t) const { return 0; }
+      } one;
+      for (int64_t q = t; q < nrows; q += nthreads) {
+        const int64_t r = rows[q];
+        SignalGroup sg{r, {}};
+        for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e)
+          sg.group.push_back(Signal{col[e], (double)val[e]});
+        int info = 0;
+        loss_out[q] = updateFactorsForOne(X, one, y, ident, sg, YtY, alpha, lambda, k, &info);
+        if (info) infos[(size_t)t] = info;
+        std::copy(X.begin(), X.end(), x_out + q * k);
+      }
+    });
+  for (auto& x : th) x.join();
+  for (int v : infos)
+    if (v) return v;
+  return 0;
+}
+
 // ---- BPR -------------------------------------------------------------------------------
 double orc_bpr_predict_difference(const double* U, const double* I, const double* bias, int k,
                                   int64_t u, int64_t p, int64_t n, int useBiases) {
@@ -642,6 +700,78 @@ double orc_bpr_loss_sum(const double* U, const double* I, const double* bias, in
 // mt19937(evalSeed) + uniform_int_distribution<int>(0, nitems − 1) with rejection.
 // Outputs: index sizes and ids, eval / test-eval triplets (u, p, n).  Returns 1 (instead
 // of spinning forever like the reference) when some user has every item as a positive.
+// One BPR epoch as BPREngine::optimize runs it with numHogwildThreads = T > 1
+// (BPREngine.cpp:146-176): T contiguous blocks of floor(N/T) positives (the tail is dropped,
+// as in the reference), each block on its own thread (iterateBlock, BPREngine-inl.h:31-46),
+// numNeg negatives per positive rejection-sampled against the user's unordered_set
+// (sampleRandomNegative, -inl.h:48-60), update() on shared rows without locks, then the
+// eval-set loss (evaluate, :246-274) by a T-way mapReduce.  The reference shares one
+// mt19937 across threads (a data race); here each thread seeds its own (seed + block), which
+// can only make this baseline faster.  CPU BASELINE ONLY: the factor races make the result
+// nondeterministic, like the reference's.  Returns the elapsed seconds of the update part
+// in *t_update and of the evaluation in *t_eval; the eval loss sum in *eval_loss.
+int orc_bpr_hogwild_epoch(double* U, double* I, double* bias, int k, const int64_t* pos_user,
+                          const int64_t* pos_item, int64_t npos, int64_t nusers, int64_t nitems,
+                          int numNeg, int nthreads, uint64_t seed, double lr, double biasLambda,
+                          double userLambda, double itemLambda, int useBiases,
+                          const int64_t* evalSet, int64_t nEval, double* t_update,
+                          double* t_eval, double* eval_loss) {
+  if (nthreads < 1) nthreads = 1;
+  // itemMap_ (BPREngine.cpp:79-82): per-user unordered_set of positive items
+  std::vector<std::unordered_set<size_t>> itemMap((size_t)nusers);
+  for (int64_t e = 0; e < npos; ++e) itemMap[(size_t)pos_user[e]].insert((size_t)pos_item[e]);
+  std::atomic<int> bad{0};
+  auto t0 = std::chrono::steady_clock::now();
+  const int64_t block = npos / nthreads;
+  auto worker = [&](int t) {
+    std::mt19937 gen((uint32_t)(seed + (uint64_t)t));
+    std::uniform_int_distribution<> dis(0, (int)nitems - 1);
+    for (int64_t i = t * block; i < (t + 1) * block; ++i) {
+      const size_t u = (size_t)pos_user[i], p = (size_t)pos_item[i];
+      const auto& set = itemMap[u];
+      for (int j = 0; j < numNeg; ++j) {
+        size_t n;
+        do {
+          n = (size_t)dis(gen);
+        } while (set.count(n) > 0);
+        const int64_t trip[3] = {(int64_t)u, (int64_t)p, (int64_t)n};
+        if (orc_bpr_update_seq(U, I, bias, k, trip, 1, lr, biasLambda, userLambda, itemLambda,
+                               useBiases))
+          bad = 1;
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+    for (auto& x : th) x.join();
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  std::vector<double> part((size_t)nthreads, 0.0);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([&, t]() {
+        double s = 0.0;
+        for (int64_t q = t; q < nEval; q += nthreads) {
+          const double x = predictDifference(U, I, bias, k, (size_t)evalSet[3 * q],
+                                             (size_t)evalSet[3 * q + 1], (size_t)evalSet[3 * q + 2],
+                                             useBiases != 0);
+          s += std::log(1.0 + std::exp(-x));
+        }
+        part[(size_t)t] = s;
+      });
+    for (auto& x : th) x.join();
+  }
+  double loss = 0.0;
+  for (double v : part) loss += v;
+  auto t2 = std::chrono::steady_clock::now();
+  *t_update = std::chrono::duration<double>(t1 - t0).count();
+  *t_eval = std::chrono::duration<double>(t2 - t1).count();
+  *eval_loss = loss;
+  return bad.load();
+}
+
 int orc_bpr_sets(const int64_t* users, const int64_t* items, const double* vals, int64_t n,
                  const int64_t* tusers, const int64_t* titems, const double* tvals, int64_t tn,
                  int64_t evalNumNeg, int32_t evalSeed, int64_t* nusers, int64_t* nitems,
