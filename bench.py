@@ -45,9 +45,20 @@ def log(*a):
 MKL = "/opt/conda/lib/libmkl_rt.so.1"
 
 
+_CPU_SHARE = None
+
+
 def cpu_share():
     """Threads for the CPU baseline: `nproc` (which honours OMP_NUM_THREADS, as the box sets
-    it to its CPU share), bounded by the affinity mask and the cgroup CPU quota."""
+    it to its CPU share), bounded by the affinity mask and the cgroup CPU quota.  Taken once,
+    before oracle_lib() sets OMP_NUM_THREADS=1 for the port."""
+    global _CPU_SHARE
+    if _CPU_SHARE is None:
+        _CPU_SHARE = _cpu_share()
+    return _CPU_SHARE
+
+
+def _cpu_share():
     import subprocess
     aff = len(os.sched_getaffinity(0))
     quota = None
@@ -331,6 +342,7 @@ def main():
 
     import qmf_amd
 
+    cpu_share()
     if args.config in BPR_CONFIGS:
         # BPR shards nothing (Hogwild across GPUs would need cross-device atomics): every
         # rank runs an independent replica; rank 0 reports

@@ -87,14 +87,18 @@ int qmfx_fill_uniform(qmfx_ctx* ctx, int side, double bound, uint64_t seed);
  * With a distributed context the local row range is solved and the factor matrix is
  * all-gathered over RCCL before returning; the loss is then the global sum. */
 int qmfx_wals_half(qmfx_ctx* ctx, int side, double alpha, double lambda, double* loss_sum);
-/* Number of rows whose system was not positive definite in the last half (a non-positive
- * Cholesky pivot: only possible when some 1 + α·v < 0 or λ ≤ 0).  Their indices are
- * written to rows[] (up to cap).  The C++ engine re-solves them on the host with an LDLᵀ
- * (Bunch-Kaufman) solve, as dsysv_ would. */
+/* Number of rows whose system the Cholesky kernels could not factor in the last half (a
+ * non-positive pivot: some 1 + α·v < 0, λ ≤ 0, or fp32 rounding on a nearly singular
+ * system); their indices go to rows[] (up to cap).  qmfx_wals_half has already re-solved
+ * them on the device in fp64 with partial pivoting (dsysv_'s role, Matrix.cpp:81-96) before
+ * the half's all-gather, and failed with -6 if one was exactly singular (CHECK(info == 0),
+ * Matrix.cpp:94). */
 int qmfx_wals_failed_rows(qmfx_ctx* ctx, int64_t* rows, int64_t cap, int64_t* count);
 /* Per-row loss terms of the last half (n_side values; the sum is *loss_sum). */
 int qmfx_wals_row_losses(qmfx_ctx* ctx, double* out);
-/* Host-side re-solve input for a failed row: A (k×k row-major, λ included) and b. */
+/* One row's system as the reference forms it (updateFactorsForOne, WALSEngine.cpp:266-299),
+ * built on the device in fp64 from the current fixed side: A (k×k row-major, λ included),
+ * b and Σ(1 + αv). */
 int qmfx_wals_row_system(qmfx_ctx* ctx, int side, int64_t row, double alpha, double lambda,
                          double* A, double* b, double* csum);
 int qmfx_wals_set_row(qmfx_ctx* ctx, int side, int64_t row, const double* x);

@@ -239,6 +239,16 @@ class Context:
         _check(lib().qmfx_wals_failed_rows(self.h, _p(rows, P_i64), cnt.value, ctypes.byref(cnt)))
         return rows[: cnt.value]
 
+    def row_system(self, side, row, alpha, lam):
+        """(A, b, Σc) of one row's k×k system, built on the device."""
+        k = self.k
+        A = np.empty((k, k), np.float64)
+        b = np.empty(k, np.float64)
+        cs = np.zeros(1, np.float64)
+        _check(lib().qmfx_wals_row_system(self.h, side, int(row), float(alpha), float(lam),
+                                          _p(A, P_f64), _p(b, P_f64), _p(cs, P_f64)))
+        return A, b, float(cs[0])
+
     def sync(self):
         _check(lib().qmfx_sync(self.h))
 

@@ -94,6 +94,33 @@ hipError_t launch_mfma_selftest_f32(const float* A, const float* B, float* C, hi
 hipError_t launch_mfma_selftest_f64(const double* A, const double* B, double* C,
                                     hipStream_t s);
 
+// Pivoted fp64 re-solve of the rows flagged in `status` (fallback.hip)
+template <typename T>
+struct FallbackArgs {
+  const int64_t* rowptr;
+  const int32_t* col;
+  const T* val;
+  const T* Y;             // fixed side [nY][kp]
+  const T* G;             // YᵀY of the fixed side, kp×kp
+  T* X;                   // solved side [nX][kp]
+  double* rowloss;
+  int32_t* status;        // in: non-zero = flagged; out: 1 re-solved, 2 singular
+  const RowDesc* desc;    // slot → row
+  int64_t slot_begin, nslots;
+  double alpha, lambda;
+  int k, kp;
+  double* scratch;        // FB_MAX_GRID × (kp + 3) × kp doubles
+  unsigned long long* counters;  // [0] rows re-solved, [1] singular rows
+};
+constexpr int FB_MAX_GRID = 64;
+hipError_t launch_wals_fallback(const FallbackArgs<float>& a, hipStream_t s);
+hipError_t launch_wals_fallback(const FallbackArgs<double>& a, hipStream_t s);
+// out: A (k×k row-major, λ included), then b (k), then Σc — one row's system
+hipError_t launch_wals_system(const FallbackArgs<float>& a, int64_t beg, int64_t end, double* out,
+                              hipStream_t s);
+hipError_t launch_wals_system(const FallbackArgs<double>& a, int64_t beg, int64_t end,
+                              double* out, hipStream_t s);
+
 // BPR (bpr.hip)
 template <typename T>
 struct BprArgs {

@@ -90,6 +90,10 @@ struct qmfx_ctx {
   double* rowloss = nullptr;
   int64_t rowloss_cap = 0;
   int32_t* status = nullptr;
+  // pivoted re-solve of flagged rows (fallback.hip): scratch and [re-solved, singular] counts
+  double* fb_scratch = nullptr;
+  unsigned long long* fb_cnt = nullptr;
+  int64_t fb_rows = 0;  // rows re-solved by the last half
   double* dsum = nullptr;
   double* hsum = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -330,6 +334,30 @@ int build_buckets(qmfx_ctx* c, int side) {
   return 0;
 }
 
+template <typename T>
+FallbackArgs<T> fallback_args(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int64_t slot_begin,
+                              int64_t nslots, double alpha, double lambda) {
+  FallbackArgs<T> a{};
+  a.rowptr = L.rowptr;
+  a.col = L.col;
+  a.val = (const T*)L.val;
+  a.Y = (const T*)R.F;
+  a.G = (const T*)c->G;
+  a.X = (T*)L.F;
+  a.rowloss = c->rowloss;
+  a.status = c->status;
+  a.desc = L.d_desc;
+  a.slot_begin = slot_begin;
+  a.nslots = nslots;
+  a.alpha = alpha;
+  a.lambda = lambda;
+  a.k = c->k;
+  a.kp = c->kp;
+  a.scratch = c->fb_scratch;
+  a.counters = c->fb_cnt;
+  return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -381,6 +409,9 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipMalloc(&c->chol_status, sizeof(int32_t));
   if (e == hipSuccess && c->kp > 128)
     e = hipMalloc(&c->chol_scratch, (size_t)c->kp * (c->kp + 1) * sizeof(double));
+  if (e == hipSuccess)
+    e = hipMalloc(&c->fb_scratch, (size_t)FB_MAX_GRID * (c->kp + 3) * c->kp * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->fb_cnt, 2 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     g_err = std::string("qmfx_create: ") + hipGetErrorString(e);
     delete c;
@@ -445,6 +476,8 @@ int qmfx_destroy(qmfx_ctx* c) {
   dfree_t(c->trace);
   dfree_t(c->chol_status);
   dfree_t(c->chol_scratch);
+  dfree_t(c->fb_scratch);
+  dfree_t(c->fb_cnt);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -764,6 +797,7 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
       HIPCHK(launch_gimg((const double*)c->G, c->nt, c->k, lambda, (double*)c->Gimg, c->stream));
   }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->fb_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
   const char* trace_path = std::getenv("QMFX_TRACE");
   if (trace_path && c->trace_cap < L.n_ord) {
     dfree_t(c->trace);
@@ -824,6 +858,15 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
         HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[4],
                              c->nt, (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
     }
+    // rows the Cholesky kernels flagged: pivoted fp64 re-solve before the all-gather
+    if (pc.n_ord > 0) {
+      if (fp32)
+        HIPCHK(launch_wals_fallback(
+            fallback_args<float>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
+      else
+        HIPCHK(launch_wals_fallback(
+            fallback_args<double>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
+    }
     HIPCHK(hipEventRecord(c->evp[j][2], c->stream));
     if (dist) {
       // piece j of every rank → every rank (an all-gather-v of contiguous row ranges), on
@@ -859,7 +902,12 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   }
   HIPCHK(hipEventRecord(c->evh[2], c->stream));
   HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  unsigned long long fb[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(fb, c->fb_cnt, sizeof(fb), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  c->fb_rows = (int64_t)fb[0];
+  // the reference's CHECK(info == 0) after dsysv_ (Matrix.cpp:94)
+  if (fb[1]) return fail(std::to_string(fb[1]) + " singular row system(s) (dsysv info > 0)", -6);
   int32_t chol_bad = 0;
   if (use_w) HIPCHK(hipMemcpy(&chol_bad, c->chol_status, 4, hipMemcpyDeviceToHost));
   if (chol_bad) return fail("YᵀY + λI is not positive definite", -5);
@@ -933,58 +981,41 @@ int qmfx_wals_failed_rows(qmfx_ctx* c, int64_t* rows, int64_t cap, int64_t* coun
 
 int qmfx_wals_row_system(qmfx_ctx* c, int side, int64_t row, double alpha, double lambda,
                          double* A, double* b, double* csum) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
   SideBuf& L = c->s[side];
   SideBuf& R = c->s[1 - side];
   if (row < 0 || row >= L.n) return fail("row out of range");
+  if (!L.rowptr) return fail("no interactions uploaded for this side");
   if (set_dev(c)) return -2;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  const int k = c->k, kp = c->kp;
-  // G of the fixed side as used by the last half: recompute to be safe
-  std::vector<double> G((size_t)kp * kp);
-  if (c->prec == 32) {
-    std::vector<float> g((size_t)kp * kp);
-    HIPCHK(scopy(c, g.data(), c->G, g.size() * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < g.size(); ++i) G[i] = g[i];
-  } else {
-    HIPCHK(scopy(c, G.data(), c->G, G.size() * 8, hipMemcpyDeviceToHost));
-  }
-  const int64_t rb = L.h_rowptr[row], re = L.h_rowptr[row + 1];
-  std::vector<int32_t> cols((size_t)(re - rb));
-  std::vector<double> vals((size_t)(re - rb));
-  if (re > rb) {
-    HIPCHK(scopy(c, cols.data(), L.col + rb, cols.size() * 4, hipMemcpyDeviceToHost));
-    if (c->prec == 32) {
-      std::vector<float> v(vals.size());
-      HIPCHK(scopy(c, v.data(), (float*)L.val + rb, v.size() * 4, hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < v.size(); ++i) vals[i] = v[i];
-    } else {
-      HIPCHK(scopy(c, vals.data(), (double*)L.val + rb, vals.size() * 8, hipMemcpyDeviceToHost));
-    }
-  }
-  for (int i = 0; i < k; ++i) {
-    b[i] = 0.0;
-    for (int j = 0; j < k; ++j) A[i * k + j] = G[(size_t)i * kp + j];
-  }
-  double cs = 0.0;
-  std::vector<double> y(k);
-  for (size_t e = 0; e < cols.size(); ++e) {
-    if (c->prec == 32) {
-      std::vector<float> yf(kp);
-      HIPCHK(scopy(c, yf.data(), (float*)R.F + (size_t)cols[e] * kp, kp * 4, hipMemcpyDeviceToHost));
-      for (int i = 0; i < k; ++i) y[i] = yf[i];
-    } else {
-      std::vector<double> yd(kp);
-      HIPCHK(scopy(c, yd.data(), (double*)R.F + (size_t)cols[e] * kp, kp * 8, hipMemcpyDeviceToHost));
-      for (int i = 0; i < k; ++i) y[i] = yd[i];
-    }
-    for (int i = 0; i < k; ++i) {
-      b[i] += y[i] * (1.0 + alpha * vals[e]);
-      for (int j = 0; j < k; ++j) A[i * k + j] += y[i] * alpha * vals[e] * y[j];
-    }
-    cs += 1.0 + alpha * vals[e];
-  }
-  for (int i = 0; i < k; ++i) A[i * k + i] += lambda;
-  if (csum) *csum = cs;
+  if (int rc = ensure_side_factors(c, 1 - side)) return rc;
+  const int k = c->k;
+  // YᵀY of this side's fixed side (the last half may have solved the other side)
+  if (c->prec == 32)
+    HIPCHK(use_big(c) ? launch_gram_big((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart,
+                                        c->gpart_blocks, c->stream)
+                      : launch_gram((const float*)R.F, R.n, c->nt, (float*)c->G, c->gpart,
+                                    c->gpart_blocks, c->stream));
+  else
+    HIPCHK(use_big(c) ? launch_gram_big((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
+                                        c->gpart_blocks, c->stream)
+                      : launch_gram((const double*)R.F, R.n, c->nt, (double*)c->G, c->gpart,
+                                    c->gpart_blocks, c->stream));
+  double* d = nullptr;
+  const size_t nout = (size_t)k * k + k + 1;
+  HIPCHK(hipMalloc(&d, nout * sizeof(double)));
+  const int64_t beg = L.h_rowptr[row], end = L.h_rowptr[row + 1];
+  hipError_t e = c->prec == 32
+                     ? launch_wals_system(fallback_args<float>(c, L, R, 0, 0, alpha, lambda), beg,
+                                          end, d, c->stream)
+                     : launch_wals_system(fallback_args<double>(c, L, R, 0, 0, alpha, lambda), beg,
+                                          end, d, c->stream);
+  std::vector<double> h(nout);
+  if (e == hipSuccess) e = scopy(c, h.data(), d, nout * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(std::string("qmfx_wals_row_system: ") + hipGetErrorString(e), -2);
+  std::copy(h.begin(), h.begin() + (size_t)k * k, A);
+  std::copy(h.begin() + (size_t)k * k, h.begin() + (size_t)k * k + k, b);
+  if (csum) *csum = h[(size_t)k * k + k];
   return 0;
 }
 

@@ -76,48 +76,22 @@ void WALSEngine::initTest(const std::vector<DatasetElem>& testDataset) {
   }
 }
 
-Double WALSEngine::resolveFailedRows(const int side) {
-  qmfx_ctx* c = dev_->get();
+void WALSEngine::reportFailedRows(const int side) {
   int64_t count = 0;
-  QMFX_CHECK(qmfx_wals_failed_rows(c, nullptr, 0, &count));
-  if (count == 0) return 0.0;
-  std::vector<int64_t> rows(static_cast<size_t>(count));
-  QMFX_CHECK(qmfx_wals_failed_rows(c, rows.data(), count, &count));
+  QMFX_CHECK(qmfx_wals_failed_rows(dev_->get(), nullptr, 0, &count));
+  if (count == 0) return;
+  // the device re-solved them in fp64 with a pivoted factorization (dsysv_'s role,
+  // Matrix.cpp:81-96) inside the half; a singular one fails qmfx_wals_half itself
   LOG(WARNING) << count << (side == QMFX_USERS ? " user" : " item")
-               << " systems are not positive definite; solving them on the host";
-  const size_t k = config_.nfactors;
-  const Double alpha = config_.confidenceWeight, lambda = config_.regularizationLambda;
-  std::vector<Double> A(k * k), b(k);
-  Double loss = 0.0;
-  for (const int64_t row : rows) {
-    Double csum = 0.0;
-    QMFX_CHECK(qmfx_wals_row_system(c, side, row, alpha, lambda, A.data(), b.data(), &csum));
-    Matrix M(k, k);
-    Vector rhs(k);
-    std::copy(A.begin(), A.end(), M.data());
-    std::copy(b.begin(), b.end(), rhs.data());
-    const Vector x = linearSymmetricSolve(M, rhs);
-    // Σ(1+αv) + xᵀ(A−λI)x − 2xᵀb (WALSEngine.cpp:300-308)
-    Double xAx = 0.0, xb = 0.0, xx = 0.0;
-    for (size_t i = 0; i < k; ++i) {
-      Double ai = 0.0;
-      for (size_t j = 0; j < k; ++j) ai += A[i * k + j] * x(j);
-      xAx += x(i) * ai;
-      xb += x(i) * b[i];
-      xx += x(i) * x(i);
-    }
-    loss += csum + xAx - lambda * xx - 2.0 * xb;
-    QMFX_CHECK(qmfx_wals_set_row(c, side, row, x.data()));
-  }
-  hostResolved_ += rows.size();
-  return loss;
+               << " systems are not positive definite; re-solved with pivoting on the device";
+  pivotedRows_ += static_cast<size_t>(count);
 }
 
 Double WALSEngine::iterate(const int side) {
   Double sum = 0.0;
   QMFX_CHECK(qmfx_wals_half(dev_->get(), side, config_.confidenceWeight,
                             config_.regularizationLambda, &sum));
-  sum += resolveFailedRows(side);
+  reportFailedRows(side);
   hostStale_ = true;
   lastLoss_ = sum / (static_cast<Double>(nusers()) * static_cast<Double>(nitems()));
   return lastLoss_;

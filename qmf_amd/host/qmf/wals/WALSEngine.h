@@ -59,17 +59,18 @@ class WALSEngine : public Engine {
   const IdIndex& itemIndex() const { return itemIndex_; }
   // the loss the last half-epoch returned (Σ row losses / (nusers · nitems))
   Double lastLoss() const { return lastLoss_; }
-  // rows re-solved on the host because their system was not positive definite
-  size_t hostResolvedRows() const { return hostResolved_; }
+  // rows re-solved with pivoting (on the device) because their system was not positive
+  // definite
+  size_t pivotedRows() const { return pivotedRows_; }
   qmfx_ctx* deviceContext() const { return dev_ ? dev_->get() : nullptr; }
 
  private:
   // one half-epoch: solve every row of `side` with the other side fixed; returns the
   // loss normalised as WALSEngine::iterate does (WALSEngine.cpp:215)
   Double iterate(int side);
-  // re-solve the rows the device flagged (non-positive Cholesky pivot) with a pivoted
-  // host solve; returns their summed loss
-  Double resolveFailedRows(int side);
+  // logs the rows of the last half whose system was not positive definite (the device
+  // re-solved them with pivoting inside the half)
+  void reportFailedRows(int side);
   void syncHost() const;
 
   const WALSConfig& config_;
@@ -90,7 +91,7 @@ class WALSEngine : public Engine {
   std::vector<RankedUser> testRanks_;
 
   Double lastLoss_ = 0.0;
-  size_t hostResolved_ = 0;
+  size_t pivotedRows_ = 0;
 };
 
 }  // namespace qmf

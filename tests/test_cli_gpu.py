@@ -108,16 +108,16 @@ def test_wals_cli_ml100k_shape_matches_reference_losses(tmp_path, precision, tol
     assert rel_err(U, o.factors(0)) < tol and rel_err(I, o.factors(1)) < tol
 
 
-def test_wals_cli_indefinite_rows_fall_back_to_host(tmp_path):
+def test_wals_cli_indefinite_rows_are_resolved(tmp_path):
     # 1 + α·v < 0 with O(1) factors makes some user systems indefinite: the device flags
-    # them and the engine re-solves them on the host with a pivoted solve, where the
-    # reference's dsysv would run Bunch-Kaufman.  One user half + one item half.
+    # them and re-solves them in fp64 with a pivoted solve, where the reference's dsysv
+    # would run Bunch-Kaufman.  One user half + one item half.
     u, i, v = synth(300, 80, 3000, seed=9)
     v = v.copy()
     v[::11] = -5.0
     init = np.random.default_rng(1).uniform(0.2, 0.4, (80, 8))
     log, ol, U, I, o = wals_vs_oracle(tmp_path, u, i, v, 8, 1, 64, lam=0.01, init=init)
-    assert "not positive definite; solving them on the host" in log
+    assert "not positive definite; re-solved with pivoting" in log
     assert rel_err(U, o.factors(0)) < 1e-7 and rel_err(I, o.factors(1)) < 1e-7
     np.testing.assert_allclose(losses(log), ol, rtol=LOG_RTOL)
 
