@@ -140,10 +140,21 @@ int qmfx_eval_ranks(qmfx_ctx* ctx, int use_biases, double* label_scores, int64_t
 
 /* ---- multi-GPU (one process per GPU; RCCL over xGMI) -------------------------------------- */
 int qmfx_rccl_unique_id(uint8_t* id128);
+/* Joins the RCCL communicator (id128 from rank 0's qmfx_rccl_unique_id), takes this rank's
+ * nnz-balanced row range of both sides, rebuilds the row buckets and keeps only this rank's
+ * signals on the device.  id128 = NULL sets up the partition without a communicator: each
+ * half then solves only this rank's rows and exchanges nothing (tests of the partition). */
 int qmfx_dist_init(qmfx_ctx* ctx, int rank, int world, const uint8_t* id128);
 /* nnz-balanced contiguous row range owned by `rank` (host-only helper, no GPU needed). */
 int qmfx_partition_rows(const int64_t* rowptr, int64_t nrows, int world, int rank,
                         int64_t* begin, int64_t* end);
+/* The all-gather schedule of a half-epoch over `world` ranks with `npieces` solve pieces
+ * per rank (host only, no device): pbounds[r·(npieces+1) + j] .. [.. + j + 1] is the row
+ * range rank r solves as its piece j and then broadcasts to every rank (an empty range is
+ * skipped).  Ranks own contiguous nnz-balanced ranges in ascending row order (the
+ * reference's bucket split, distributed/scheduler/RunOneTask.cpp:160-243). */
+int qmfx_dist_plan(const int64_t* rowptr, int64_t nrows, int world, int npieces,
+                   int64_t* pbounds);
 
 /* ---- measurement -------------------------------------------------------------------------- */
 /* HIP-event time of the row-solve kernel launches (on the context stream) since reset. */

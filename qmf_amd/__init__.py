@@ -7,7 +7,7 @@ The product is the C ABI in ``include/qmfx.h`` implemented by ``qmf_amd/_build/l
 GPU is present the calls fail loudly.
 """
 from ._abi import (  # noqa: F401
-    LIB_PATH, QmfxError, Context, build, lib, partition_rows, rccl_unique_id, selftest_mfma,
+    LIB_PATH, QmfxError, Context, build, dist_plan, lib, partition_rows, rccl_unique_id, selftest_mfma,
     version,
 )
 

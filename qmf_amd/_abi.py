@@ -56,6 +56,7 @@ SIGNATURES = {
     "qmfx_rccl_unique_id": [P_u8],
     "qmfx_dist_init": [vp, c_int, c_int, P_u8],
     "qmfx_partition_rows": [P_i64, c_i64, c_int, c_int, P_i64, P_i64],
+    "qmfx_dist_plan": [P_i64, c_i64, c_int, c_int, P_i64],
     "qmfx_solve_kernel_stats": [vp, P_f64, P_i64, P_f64, P_f64],
     "qmfx_kernel_stats": [vp, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_reset_stats": [vp],
@@ -124,6 +125,14 @@ def partition_rows(rowptr, world, rank):
     _check(lib().qmfx_partition_rows(_p(rp, P_i64), len(rp) - 1, world, rank, ctypes.byref(b),
                                      ctypes.byref(e)))
     return b.value, e.value
+
+
+def dist_plan(rowptr, world, npieces):
+    """[world][npieces + 1] piece boundaries of the half-epoch all-gather schedule."""
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    out = np.zeros((world, npieces + 1), np.int64)
+    _check(lib().qmfx_dist_plan(_p(rp, P_i64), len(rp) - 1, world, npieces, _p(out, P_i64)))
+    return out
 
 
 class Context:
@@ -309,7 +318,9 @@ class Context:
 
     # ---- dist / stats
     def dist_init(self, rank, world, uid):
-        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        """uid = rank 0's rccl_unique_id(), or None: partition and shard without a
+        communicator (each half solves only this rank's rows)."""
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid) if uid is not None else None
         _check(lib().qmfx_dist_init(self.h, rank, world, buf))
 
     def solve_stats(self):

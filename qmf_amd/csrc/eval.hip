@@ -60,10 +60,12 @@ __global__ __launch_bounds__(256) void eval_label_kernel(EvalArgs<T> a) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void eval_users_kernel(EvalArgs<T> a) {
-  // layout [t / 8][f][t % 8]: one wave's 8 users at factor f are 64 contiguous bytes
-  const int64_t t = blockIdx.x;
+  // layout [t / 8][f][t % 8] (t relative to the batch's first user): one wave's 8 users at
+  // factor f are 64 contiguous bytes
+  const int64_t tr = blockIdx.x;
+  const int64_t t = a.t_base + tr;
   const T* u = a.U + (t < a.ntest ? a.users[t] * (int64_t)a.kp : 0);
-  double* o = a.udbl + (t / EV_UW) * a.k * EV_UW + (t % EV_UW);
+  double* o = a.udbl + (tr / EV_UW) * a.k * EV_UW + (tr % EV_UW);
   for (int f = threadIdx.x; f < a.k; f += blockDim.x)
     o[f * EV_UW] = t < a.ntest ? (double)u[f] : 0.0;
 }
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(EvalArgs<T> a) {
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t t0 = (int64_t)blockIdx.y * EV_UG;
+  const int64_t t0 = a.t_base + (int64_t)blockIdx.y * EV_UG;
   const int64_t tw = t0 + w * EV_UW;  // first user of this wave
   const int64_t i0 = (int64_t)blockIdx.x * a.chunk;
   const int64_t i1 = i0 + a.chunk < a.nitems ? i0 + a.chunk : a.nitems;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(EvalArgs<T> a) {
   // wave-uniform rows, read through the constant address space so they become scalar loads
   // (the kernel's own global stores would otherwise keep them on the vector path)
   typedef const __attribute__((address_space(4))) double* cdptr;
-  const cdptr ud = (cdptr)(a.udbl + tw * a.k);  // [f][8] for this wave's users
+  const cdptr ud = (cdptr)(a.udbl + (tw - a.t_base) * a.k);  // [f][8] for this wave's users
   const cdptr ps = (cdptr)a.pscore;  // written by eval_label_kernel (an earlier launch)
   typedef const __attribute__((address_space(4))) int64_t* ciptr;
   const ciptr pp = (ciptr)a.pptr;
@@ -180,18 +182,40 @@ hipError_t eval_ranks(const EvalArgs<T>& a0, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a.ntest == 0 || a.nitems == 0) return e;
   const int64_t groups = (a.ntest + EV_UG - 1) / EV_UG;
-  hipLaunchKernelGGL(eval_users_kernel<T>, dim3((unsigned)(groups * EV_UG)), dim3(256), 0, s, a);
   const int64_t nchunk = eval_chunks(a.ntest, a.nitems);
   a.chunk = ((a.nitems + nchunk - 1) / nchunk + EV_TI - 1) / EV_TI * EV_TI;
-  if (groups > 65535) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(eval_rank_kernel<T>, dim3((unsigned)nchunk, (unsigned)groups), dim3(256),
-                     0, s, a);
-  return hipGetLastError();
+  // test users in batches of eval_batch_groups() groups (grid.y ≤ 65535; the users' fp64
+  // rows in udbl are staged per batch)
+  const int64_t bg = eval_batch_groups();
+  for (int64_t g0 = 0; g0 < groups; g0 += bg) {
+    const int64_t ng = groups - g0 < bg ? groups - g0 : bg;
+    a.t_base = g0 * EV_UG;
+    hipLaunchKernelGGL(eval_users_kernel<T>, dim3((unsigned)(ng * EV_UG)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(eval_rank_kernel<T>, dim3((unsigned)nchunk, (unsigned)ng), dim3(256), 0,
+                       s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace
 
-int64_t eval_user_rows(int64_t ntest) { return (ntest + EV_UG - 1) / EV_UG * EV_UG; }
+// User groups (of EV_UG test users) per rank-kernel launch: the grid's y limit
+// (QMFX_EVAL_BATCH_GROUPS lowers it for the tests).
+int64_t eval_batch_groups() {
+  int64_t g = 65535;
+  if (const char* e = std::getenv("QMFX_EVAL_BATCH_GROUPS"))
+    if (std::atoll(e) > 0 && std::atoll(e) < g) g = std::atoll(e);
+  return g;
+}
+
+// rows of the per-batch fp64 user scratch (udbl)
+int64_t eval_user_rows(int64_t ntest) {
+  const int64_t rows = (ntest + EV_UG - 1) / EV_UG * EV_UG;
+  const int64_t cap = eval_batch_groups() * EV_UG;
+  return rows < cap ? rows : cap;
+}
 
 // Item chunks per user group: about 4096 workgroups over the grid, ≥ one tile per chunk.
 // The host sizes the Σ score² partial buffer [chunks][ntest] with the same function.

@@ -209,11 +209,13 @@ struct EvalArgs {
   double* pscore;           // [npos] scores (written by the label pass)
   unsigned long long* above;  // [npos] items scored strictly higher (zeroed by the caller)
   double* sq_part;          // [eval_chunks(ntest, nitems)][ntest] Σ score² per item chunk
-  double* udbl;             // [eval_user_rows(ntest)][k] scratch: test users' rows as doubles
+  double* udbl;             // [eval_user_rows(ntest)][k] scratch: one batch's test users' rows
   int64_t chunk;            // set by the launcher
+  int64_t t_base;           // set by the launcher: first test user of the current batch
 };
 int64_t eval_chunks(int64_t ntest, int64_t nitems);
 int64_t eval_user_rows(int64_t ntest);
+int64_t eval_batch_groups();
 hipError_t launch_eval_ranks(const EvalArgs<float>& a, hipStream_t s);
 hipError_t launch_eval_ranks(const EvalArgs<double>& a, hipStream_t s);
 

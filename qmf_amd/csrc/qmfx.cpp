@@ -52,6 +52,11 @@ struct SideBuf {
   std::vector<int64_t> h_rowptr;
   std::vector<int64_t> h_ids;           // ascending ids (only when built by qmfx_group_signals)
   int64_t rbeg = 0, rend = 0;           // rows solved by this rank
+  // With several ranks the CSR keeps only this rank's rows (signals rowptr[rbeg] ..
+  // rowptr[rend]); col/val point at that shard and shard_off = rowptr[rbeg], so kernels
+  // index them with the global rowptr through colp()/valp().
+  int64_t shard_off = 0;
+  bool sharded = false;
   std::vector<int64_t> bounds;          // per-rank row boundaries (world+1)
   // Row buckets of this rank (device list `order`): [whitened n≤16 | ≤32 | ≤48 | ≤64 |
   // direct rows, heaviest first].  wb[i]..wb[i+1] = whitened bucket NTN = i+1; wb[4]..n_ord
@@ -73,6 +78,20 @@ struct SideBuf {
   std::vector<Piece> pieces;
   std::vector<int64_t> pbounds;  // world × (npieces + 1): piece boundaries of every rank
 };
+
+int32_t* colp(const SideBuf& sb) { return sb.col - sb.shard_off; }
+template <typename T>
+const T* valp(const SideBuf& sb) {
+  return (const T*)sb.val - sb.shard_off;
+}
+// frees the CSR arrays of a side (all of them, or only col/val)
+void drop_csr(SideBuf& sb, bool rowptr_too) {
+  if (rowptr_too && sb.rowptr) (void)hipFree(sb.rowptr), sb.rowptr = nullptr;
+  if (sb.col) (void)hipFree(sb.col), sb.col = nullptr;
+  if (sb.val) (void)hipFree(sb.val), sb.val = nullptr;
+  sb.shard_off = 0;
+  sb.sharded = false;
+}
 
 }  // namespace
 
@@ -260,6 +279,18 @@ void split_rows(const std::vector<int64_t>& rp, int64_t b, int64_t e, int p, int
   }
 }
 
+// The all-gather schedule of a half: rank r owns rows [bounds[r], bounds[r+1]) and splits
+// them into P nnz-balanced pieces; pb[r·(P+1) + j] .. pb[r·(P+1) + j + 1] is the row range
+// rank r broadcasts after solving its piece j (qmfx_wals_half), skipped when empty.
+void plan_pieces(const std::vector<int64_t>& rp, const std::vector<int64_t>& bounds, int world,
+                 int P, std::vector<int64_t>& pb) {
+  pb.assign((size_t)world * (P + 1), 0);
+  for (int r = 0; r < world; ++r) split_rows(rp, bounds[r], bounds[r + 1], P, &pb[(size_t)r * (P + 1)]);
+}
+
+// Keeps only this rank's signals of a side on the device (col/val of rows rbeg..rend).
+int shard_csr(qmfx_ctx* c, SideBuf& sb);
+
 // Splits this rank's rows of `side` into pieces, and each piece into whitened buckets (by
 // padded signal count) and the direct bucket (heaviest rows first, for load balance);
 // uploads the order list (piece sections back to back) and the per-slot descriptors.
@@ -270,9 +301,7 @@ int build_buckets(qmfx_ctx* c, int side) {
   if (sb.n > INT32_MAX) return fail("more than 2^31 rows on one side are not supported");
   const int mx = max_whitened_ntn(c);
   const int P = npieces(c);
-  sb.pbounds.assign((size_t)c->world * (P + 1), 0);
-  for (int r = 0; r < c->world; ++r)
-    split_rows(sb.h_rowptr, sb.bounds[r], sb.bounds[r + 1], P, &sb.pbounds[(size_t)r * (P + 1)]);
+  plan_pieces(sb.h_rowptr, sb.bounds, c->world, P, sb.pbounds);
   double nnz_w = 0, nnz_d = 0, flops_w = 0;
   const double k = c->k;
   std::vector<int64_t> order;
@@ -334,13 +363,37 @@ int build_buckets(qmfx_ctx* c, int side) {
   return 0;
 }
 
+int shard_csr(qmfx_ctx* c, SideBuf& sb) {
+  if (sb.sharded || !sb.col) return 0;
+  const int64_t e0 = sb.h_rowptr[sb.rbeg], e1 = sb.h_rowptr[sb.rend];
+  const size_t m = (size_t)std::max<int64_t>(e1 - e0, 1);
+  int32_t* col = nullptr;
+  void* val = nullptr;
+  HIPCHK(hipMalloc(&col, m * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&val, m * c->esz));
+  if (e1 > e0) {
+    HIPCHK(hipMemcpyAsync(col, sb.col + e0, (size_t)(e1 - e0) * sizeof(int32_t),
+                          hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(val, (char*)sb.val + (size_t)e0 * c->esz, (size_t)(e1 - e0) * c->esz,
+                          hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  (void)hipFree(sb.col);
+  (void)hipFree(sb.val);
+  sb.col = col;
+  sb.val = val;
+  sb.shard_off = e0;
+  sb.sharded = true;
+  return 0;
+}
+
 template <typename T>
 FallbackArgs<T> fallback_args(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int64_t slot_begin,
                               int64_t nslots, double alpha, double lambda) {
   FallbackArgs<T> a{};
   a.rowptr = L.rowptr;
-  a.col = L.col;
-  a.val = (const T*)L.val;
+  a.col = colp(L);
+  a.val = valp<T>(L);
   a.Y = (const T*)R.F;
   a.G = (const T*)c->G;
   a.X = (T*)L.F;
@@ -434,9 +487,7 @@ int qmfx_destroy(qmfx_ctx* c) {
   if (c->ev_sum) (void)hipEventDestroy(c->ev_sum);
   if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
   for (auto& sb : c->s) {
-    dfree_t(sb.rowptr);
-    dfree_t(sb.col);
-    dfree(sb.val);
+    drop_csr(sb, true);
     dfree(sb.F);
     dfree_t(sb.d_order);
     dfree_t(sb.d_desc);
@@ -498,9 +549,7 @@ int qmfx_set_shape(qmfx_ctx* c, int64_t nusers, int64_t nitems) {
     c->s[side].h_ids.clear();
     if (c->s[side].n != n) {
       dfree(c->s[side].F);
-      dfree_t(c->s[side].rowptr);
-      dfree_t(c->s[side].col);
-      dfree(c->s[side].val);
+      drop_csr(c->s[side], true);
       c->s[side].h_rowptr.clear();
       c->s[side].n = n;
     }
@@ -528,9 +577,7 @@ int qmfx_upload_csr(qmfx_ctx* c, int side, const int64_t* rowptr, const int32_t*
   for (int64_t e = 0; e < nnz; ++e)
     if (colidx[e] < 0 || colidx[e] >= nother) return fail("column index out of range");
   if (set_dev(c)) return -2;
-  dfree_t(sb.rowptr);
-  dfree_t(sb.col);
-  dfree(sb.val);
+  drop_csr(sb, true);
   HIPCHK(hipMalloc(&sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t)));
   HIPCHK(hipMalloc(&sb.col, (size_t)std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
   HIPCHK(hipMalloc(&sb.val, (size_t)std::max<int64_t>(nnz, 1) * c->esz));
@@ -581,9 +628,7 @@ int qmfx_group_signals(qmfx_ctx* c, const void* records, int64_t nnz, int64_t* n
   }
   for (int side = 0; side < 2; ++side) {
     SideBuf& sb = c->s[side];
-    dfree_t(sb.rowptr);
-    dfree_t(sb.col);
-    dfree(sb.val);
+    drop_csr(sb, true);
     sb.rowptr = o.rowptr[side];
     sb.col = o.col[side];
     sb.val = o.val[side];
@@ -622,6 +667,7 @@ int qmfx_get_ids(qmfx_ctx* c, int side, int64_t* ids) {
 int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, float* values) {
   SideBuf& sb = c->s[side];
   if (!sb.rowptr) return fail("no CSR for this side");
+  if (sb.sharded) return fail("the CSR is sharded over ranks (qmfx_dist_init): only this rank's rows are held");
   if (set_dev(c)) return -2;
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(scopy(c, rowptr, sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -653,9 +699,7 @@ int qmfx_gen_synthetic(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz,
   HIPCHK(sort_unique_keys(keys, scratch, nnz, &m, end_bit, c->stream));
   for (int side = 0; side < 2; ++side) {
     SideBuf& sb = c->s[side];
-    dfree_t(sb.rowptr);
-    dfree_t(sb.col);
-    dfree(sb.val);
+    drop_csr(sb, true);
     HIPCHK(hipMalloc(&sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t)));
     HIPCHK(hipMalloc(&sb.col, (size_t)m * sizeof(int32_t)));
     HIPCHK(hipMalloc(&sb.val, (size_t)m * c->esz));
@@ -817,14 +861,14 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     HIPCHK(hipEventRecord(c->evp[j][0], c->stream));
     if (nd > 0) {
       if (fp32) {
-        SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)R.F,
+        SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)R.F,
                            (const float*)c->G, (float*)L.F, c->rowloss, c->status, L.d_order,
                            d0, nd, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc,
                            (const float*)c->Gimg, trace_path ? c->trace : nullptr,
                            (int32_t)R.n};
         HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
       } else {
-        SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)R.F,
+        SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)R.F,
                             (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
                             d0, nd, alpha, lambda, c->k, c->ablate, L.d_desc,
                             (const double*)c->Gimg, nullptr, (int32_t)R.n};
@@ -838,13 +882,13 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
         const int64_t cnt = pc.wb[b + 1] - pc.wb[b];
         if (cnt <= 0) continue;
         if (fp32) {
-          SolveArgs<float> a{L.rowptr, L.col, (const float*)L.val, (const float*)c->Z, nullptr,
+          SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)c->Z, nullptr,
                              (float*)L.F, c->rowloss, c->status, L.d_order, pc.ord + pc.wb[b],
                              cnt, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
                              trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
           HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
         } else {
-          SolveArgs<double> a{L.rowptr, L.col, (const double*)L.val, (const double*)c->Z,
+          SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)c->Z,
                               nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
                               pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
                               nullptr, nullptr, (int32_t)c->z_cap};
@@ -986,6 +1030,7 @@ int qmfx_wals_row_system(qmfx_ctx* c, int side, int64_t row, double alpha, doubl
   SideBuf& R = c->s[1 - side];
   if (row < 0 || row >= L.n) return fail("row out of range");
   if (!L.rowptr) return fail("no interactions uploaded for this side");
+  if (L.sharded && (row < L.rbeg || row >= L.rend)) return fail("row not held by this rank");
   if (set_dev(c)) return -2;
   if (int rc = ensure_side_factors(c, 1 - side)) return rc;
   const int k = c->k;
@@ -1263,7 +1308,7 @@ int qmfx_bpr_eval(qmfx_ctx* c, int slot, const int64_t* trip, int64_t n, int use
 int qmfx_eval_set_labels(qmfx_ctx* c, int64_t ntest, const int64_t* users, const int64_t* rowptr,
                          const int64_t* items, const double* values) {
   if (!c->s[0].F || !c->s[1].F) return fail("factors not allocated (qmfx_set_shape first)");
-  if (ntest < 0 || ntest > (int64_t)65535 * 16) return fail("ntest out of range");
+  if (ntest < 0) return fail("ntest out of range");
   if (c->k > 256) return fail("evaluation supports nfactors <= 256");
   if (set_dev(c)) return -2;
   const int64_t nu = c->s[0].n, ni = c->s[1].n;
@@ -1382,7 +1427,7 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
   if (set_dev(c)) return -2;
   c->rank = rank;
   c->world = world;
-  if (world > 1) {
+  if (world > 1 && id128) {
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
@@ -1391,9 +1436,26 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
   for (int side = 0; side < 2; ++side) {
     SideBuf& sb = c->s[side];
     if (sb.h_rowptr.empty()) continue;
+    if (sb.sharded) return fail("qmfx_dist_init: the CSR is already sharded (re-upload it first)");
     set_default_bounds(sb, world, rank);
     if (int rc = build_buckets(c, side)) return rc;
+    if (world > 1)
+      if (int rc = shard_csr(c, sb)) return rc;
   }
+  return 0;
+}
+
+int qmfx_dist_plan(const int64_t* rowptr, int64_t nrows, int world, int npieces,
+                   int64_t* pbounds) {
+  if (world < 1) return fail("bad world size");
+  if (npieces < 1 || npieces > QMFX_MAX_PIECES) return fail("npieces out of range");
+  SideBuf sb;
+  sb.n = nrows;
+  sb.h_rowptr.assign(rowptr, rowptr + nrows + 1);
+  set_default_bounds(sb, world, 0);
+  std::vector<int64_t> pb;
+  plan_pieces(sb.h_rowptr, sb.bounds, world, npieces, pb);
+  std::copy(pb.begin(), pb.end(), pbounds);
   return 0;
 }
 

@@ -1,8 +1,10 @@
 """Multi-GPU decomposition, rehearsed on CPU with torch.distributed gloo (world_size 2 and
 3): each rank solves its nnz-balanced contiguous row range (qmfx_partition_rows, the
-product's partitioner; the oracle stands in for the device solve), the solved ranges are
-all-gathered and the loss all-reduced — the exchange qmfx_wals_half does with RCCL
-(grouped ncclBroadcast per rank range + ncclAllReduce).  The assembled
+product's partitioner), split into the product's solve pieces (qmfx_dist_plan, the same
+code qmfx_wals_half runs), solved piece by piece (the oracle stands in for the device
+solve), each piece broadcast by its owner and the loss all-reduced — the exchange
+qmfx_wals_half does with RCCL (grouped ncclBroadcast per piece and rank + ncclAllReduce,
+DESIGN.md §6).  The assembled
 factors must equal the single-process solve bit for bit (rows are independent given the
 fixed side), and the loss to rounding."""
 import os
@@ -52,23 +54,13 @@ def _solve_range(side, csr, n_other, fixed, b, e):
     return o.factors(side), loss
 
 
-def _allgather_rows(local, b, e, n, world):
-    """All-gather-v of contiguous row ranges (what the grouped broadcasts do)."""
-    counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(counts, torch.tensor([b, e], dtype=torch.int64))
-    mx = max(int(c[1] - c[0]) for c in counts)
-    buf = torch.zeros((mx, local.shape[1]), dtype=torch.float64)
-    buf[: e - b] = torch.from_numpy(local)
-    bufs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf)
-    out = np.zeros((n, local.shape[1]))
-    for c, t in zip(counts, bufs):
-        cb, ce = int(c[0]), int(c[1])
-        out[cb:ce] = t[: ce - cb].numpy()
-    return out
+P = 4  # solve pieces per rank (qmfx_wals_half's default with several ranks)
 
 
 def _worker(rank, world, port, result_q):
+    """One rank of qmfx_wals_half's multi-GPU schedule: for each piece j, solve this rank's
+    rows of piece j, then every rank r broadcasts its piece-j rows (skipped when empty) —
+    the grouped ncclBroadcast loop, here over gloo; then the loss all-reduce."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -77,16 +69,49 @@ def _worker(rank, world, port, result_q):
         out = {}
         fixed = init
         for side, csr, n, n_other in ((0, ucsr, nu, ni), (1, icsr, ni, nu)):
-            b, e = qmf_amd.partition_rows(csr[0], world, rank)
-            local, loss = _solve_range(side, csr, n_other, fixed, b, e)
-            full = _allgather_rows(local, b, e, n, world)
+            plan = qmf_amd.dist_plan(csr[0], world, P)
+            replica = np.full((n, K), np.nan)  # every row must be written by the exchange
+            sends = np.zeros(n, np.int64)
+            loss = 0.0
+            for j in range(P):
+                b, e = int(plan[rank, j]), int(plan[rank, j + 1])
+                if e > b:
+                    local, l = _solve_range(side, csr, n_other, fixed, b, e)
+                    replica[b:e] = local
+                    loss += l
+                for r in range(world):
+                    rb, re = int(plan[r, j]), int(plan[r, j + 1])
+                    if re <= rb:
+                        continue
+                    t = torch.from_numpy(np.ascontiguousarray(replica[rb:re]))
+                    dist.broadcast(t, src=r)
+                    replica[rb:re] = t.numpy()
+                    sends[rb:re] += 1
             t = torch.tensor([loss], dtype=torch.float64)
             dist.all_reduce(t)
-            out[side] = (full, float(t[0]) / (nu * ni), int(csr[0][e] - csr[0][b]))
-            fixed = full
+            b, e = qmf_amd.partition_rows(csr[0], world, rank)
+            out[side] = (replica, float(t[0]) / (nu * ni), int(csr[0][e] - csr[0][b]), sends)
+            fixed = replica
         result_q.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+def test_plan_covers_rows_once_in_owner_order():
+    """qmfx_dist_plan: per rank, P contiguous pieces inside the rank's partition_rows range;
+    over all ranks every row exactly once, ascending; empty ranks/pieces allowed."""
+    for rp in (np.array([0, 5, 5, 9, 30, 31]), np.array([0, 1000]), np.array([0, 0, 0, 0]),
+               np.concatenate([[0], np.cumsum(np.random.default_rng(1).integers(0, 50, 997))])):
+        for world in (1, 2, 3, 8):
+            plan = qmf_amd.dist_plan(rp, world, P)
+            n = len(rp) - 1
+            assert plan[0, 0] == 0 and plan[-1, -1] == n
+            flat = plan[:, :].ravel()
+            assert np.all(np.diff(flat) >= 0)  # ascending: pieces and ranks in row order
+            for r in range(world):
+                assert tuple(qmf_amd.partition_rows(rp, world, r)) == (plan[r, 0], plan[r, -1])
+                if r + 1 < world:
+                    assert plan[r, -1] == plan[r + 1, 0]
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -109,8 +134,10 @@ def test_sharded_half_epochs_equal_single_process(world):
         ref[side] = (o.iterate(side), o.factors(side))
     for r in range(world):
         for side in (0, 1):
-            full, loss, _ = res[r][side]
-            # every rank holds the same, complete factor matrix, equal to the 1-process one
+            full, loss, _, sends = res[r][side]
+            # every row arrived exactly once per half (from its owner's broadcast) ...
+            assert np.all(sends == 1), (r, side)
+            # ... and every rank holds the same complete factor matrix as 1 process
             assert np.array_equal(full, ref[side][1]), (r, side)
             assert abs(loss - ref[side][0]) <= 1e-12 * abs(ref[side][0])
     # the shards are nnz-balanced

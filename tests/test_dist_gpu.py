@@ -1,0 +1,54 @@
+"""The multi-GPU partition on one GPU: `world` contexts, each set up as one rank by
+qmfx_dist_init without a communicator (its nnz-balanced row range of both sides, the
+solve pieces of the all-gather schedule, and only its own signals kept on the device).
+Each half, every context solves only its rows; the test assembles the ranks' ranges (the
+all-gather the RCCL path does) and checks the result and the summed loss against the
+oracle's single-process half (WALSEngine::iterate, WALSEngine.cpp:165-218)."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+import qmf_amd
+from helpers import csr_from_triples, rel_err, synth
+
+pytestmark = pytest.mark.gpu
+LAM, ALPHA = 0.05, 40.0
+
+
+@pytest.mark.parametrize("k,precision,world", [(16, 64, 2), (16, 64, 3), (128, 32, 2),
+                                               (128, 64, 2), (256, 32, 3)])
+def test_partitioned_ranks_assemble_the_full_half(k, precision, world):
+    u, i, v = synth(3000, 600, 60000, seed=k + world)
+    v = v.copy()
+    v[::97] = -3.0  # a few indefinite rows: the pivoted re-solve runs on sharded signals
+    o = po.OracleWALS(u, i, v, k, LAM, ALPHA)
+    uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
+    init = np.random.default_rng(2).uniform(-0.01, 0.01, (len(iids), k))
+    o.set_factors(1, init)
+    ranks = []
+    for r in range(world):
+        c = qmf_amd.Context(k, precision)
+        c.set_shape(len(uids), len(iids))
+        c.upload_csr(0, *ucsr)
+        c.upload_csr(1, *icsr)
+        c.set_factors(1, init)
+        c.dist_init(r, world, None)
+        ranks.append(c)
+    with pytest.raises(qmf_amd.QmfxError, match="sharded"):
+        ranks[0].download_csr(0)
+    # fp64: 1e-7, not 1e-9 — the indefinite rows' pivoted solves amplify rounding by cond(A)
+    tol = 1e-7 if precision == 64 else 1e-4
+    for side, csr in ((0, ucsr), (1, icsr)):
+        lo = o.iterate(side)
+        ld = sum(c.wals_half(side, ALPHA, LAM) for c in ranks) / (o.nusers * o.nitems)
+        plan = qmf_amd.dist_plan(csr[0], world, 4)
+        full = np.zeros_like(o.factors(side))
+        for r, c in enumerate(ranks):
+            b, e = plan[r, 0], plan[r, -1]
+            full[b:e] = c.factors(side)[b:e]
+        assert rel_err(full, o.factors(side)) < tol, side
+        assert abs(ld - lo) < tol * abs(lo), side
+        for c in ranks:  # the all-gather
+            c.set_factors(side, full)
+    for c in ranks:
+        c.close()

@@ -98,3 +98,26 @@ def test_eval_requires_labels():
         with pytest.raises(qmf_amd.QmfxError):
             c._ev = (0, 0, 0)
             c.eval_ranks()
+
+
+@pytest.mark.parametrize("batch_groups", ["1", "3"])
+def test_eval_user_batches_equal_one_launch(batch_groups, monkeypatch):
+    """Test users beyond one launch's grid (65535 groups of 32 users, ≈2.1M users: the
+    reference's --num_test_users=0 on a C3-size set) run in batches; forcing batches of 1
+    and 3 groups on 150 users (5 groups, a ragged last one) must give the same statistics
+    bit for bit as a single launch."""
+    rng = np.random.default_rng(9)
+    nu, ni, k, ntest = 400, 900, 48, 150
+    U, I, users, rowptr, items, values = _case(rng, nu, ni, k, ntest)
+    out = []
+    for env in (None, batch_groups):
+        if env:
+            monkeypatch.setenv("QMFX_EVAL_BATCH_GROUPS", env)
+        with qmf_amd.Context(k, 64) as c:
+            c.set_shape(nu, ni)
+            c.set_factors(0, U)
+            c.set_factors(1, I)
+            c.eval_set_labels(users, rowptr, items, values)
+            out.append(c.eval_ranks())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
