@@ -253,8 +253,12 @@ bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; 
 
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
-  // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) only
-  if (use_big(c)) return c->prec == 32 && c->nt == 16 ? 4 : 0;
+  // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) and fp64
+  // k = 80..128 (NT = 5..8, the multi-wave whitened kernel)
+  if (use_big(c)) {
+    if (c->prec == 32) return c->nt == 16 ? 4 : 0;
+    return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
+  }
   int m = c->nt / 2;
   if (m > 4) m = 4;
   if (c->prec == 64 && m > 2) m = 2;

@@ -141,7 +141,21 @@ __device__ __forceinline__ void lds_row_store(T* dst, const T (&v)[16]) {
   }
 }
 
-template <typename T, int NT>
+// LDS ordering inside chol_solve: the whole workgroup when it is one wave (WS = false), or
+// only the calling wave (WS = true: one wave of a multi-wave workgroup runs the solve; LDS
+// accesses of one wave execute in order, so draining them and pinning the compiler's order
+// is enough).
+template <bool WS>
+__device__ __forceinline__ void csync() {
+  if constexpr (WS) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+template <typename T, int NT, bool WS = false>
 __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
                                            CholShared<T, NT>& S, int lane, int& bad) {
   using M = Mfma<T>;
@@ -160,7 +174,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
       for (int r = 0; r < 4; ++r)
         S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[t][r];
     }
-    __syncthreads();
+    csync<WS>();
     T pa[SLOTS][16];
     T pb[SLOTS];
 #pragma unroll
@@ -234,7 +248,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
       if (q < R) lds_row_store(&S.panel[q * PLD], pa[s]);
       if (q >= 16 && q < R) S.bw[16 * p + q] = pb[s];
     }
-    __syncthreads();
+    csync<WS>();
     // diagonal block → Lt (transposed, scaled by the column's 1/L[q][q], zero on and above
     // the diagonal)
 #pragma unroll
@@ -262,7 +276,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
         for (int s = 0; s < 4; ++s) acc[tj] = M::mma(-fr[I][s], fr[J][s], acc[tj]);
       }
     }
-    __syncthreads();
+    csync<WS>();
   }
   // backward solve Lᵀ x = y by 16-blocks from the bottom: lane cl carries row cl of the
   // block scaled by its own 1/L[cl][cl]; column c then finishes x_c (readlane) and
@@ -284,7 +298,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
 #pragma unroll
     for (int c = 15; c >= 0; --c) vm -= lt[c] * readlane(vm, c);
     if (lane < 16) S.xs[16 * I + lane] = vm;
-    __syncthreads();
+    csync<WS>();
   }
 }
 
@@ -890,6 +904,263 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Whitened row kernel, multi-wave: the same n×n solve as wals_woodbury_kernel for factor
+// counts whose whitened rows do not fit one wave's registers (fp64 k > 64, fp32 k = 256).
+// One workgroup of NWK waves per row; wave w holds the column blocks q = w·KW .. w·KW+KW-1
+// of the row's whitened rows Zₛ (same per-lane MFMA operand order as the one-wave kernel),
+// so each wave gathers 1/NWK of every signal's row and computes K = Zₛ Zₛᵀ over its columns.
+// The partial K tiles are summed in fixed order ((w0 + w2) + (w1 + w3)) through LDS into
+// wave 0, which solves the n×n system alone (chol_solve with wave-local LDS ordering); u
+// goes back through LDS and every wave forms x' = Zₛᵀu for its own columns.
+// ---------------------------------------------------------------------------------------
+template <typename T, int NTK, int NTN, int NWK>
+struct MwCfg {
+  static constexpr int KW = (NTK + NWK - 1) / NWK;  // column blocks of 16 per wave
+  static constexpr int NTT = NTN * (NTN + 1) / 2;
+};
+
+template <typename T, int NTK, int NTN, int NWK>
+__global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs<T> a) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  using v4 = typename M::acc_t;
+  using C = MwCfg<T, NTK, NTN, NWK>;
+  constexpr int KP = 16 * NTK;
+  constexpr int KW = C::KW;
+  constexpr int NTT = C::NTT;
+  static_assert(NWK == 2 || NWK == 4, "wave count");
+  __shared__ __attribute__((aligned(16))) CholShared<T, NTN> S;
+  __shared__ __attribute__((aligned(16))) acc_t red[NWK / 2][NTT][64];
+  __shared__ T gq[NWK][16 * NTN];
+  __shared__ double xbp[NWK];
+  __shared__ int sbad;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
+  const int64_t row = dn.row;
+  const int n = dn.n;  // ≤ 16·NTN by bucketing
+
+  // signal e = lane (every wave holds the same copy)
+  const bool mine = lane < n;
+  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
+  const T vr = mine ? a.val[dn.beg + lane] : T(0);
+  const T wl = mine ? a.alpha * vr : T(0);
+  const T cwl = mine ? T(1) + a.alpha * vr : T(0);
+  const bool isP = mine && wl > T(0);
+  const bool isQ = mine && wl == T(0);
+  const uint64_t mQ = __ballot(isQ);
+  const uint64_t mP = __ballot(isP);
+  const bool hasQ = mQ != 0;
+
+  // this wave's column blocks of Zₛ: zr[I][j] = z_{16I+cl}[16q + 4kk .. +3], q = wv·KW + j
+  v4 zr[NTN][KW];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int ce = __shfl(cr, 16 * I + cl, 64);
+    const v4* zrow = reinterpret_cast<const v4*>(a.Y + (uint64_t)(uint32_t)ce * KP) + kk;
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+      const int q = wv * KW + j;
+      zr[I][j] = q < NTK ? zrow[4 * q] : v4{};
+    }
+  }
+  // partial K over this wave's columns
+  acc_t acc[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
+  if constexpr (sizeof(T) == 4) {
+    constexpr int NS = (KW + 1) / 2;
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) {
+      Split3 sp[NTN];
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        float x[8];
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          x[c4] = zr[I][2 * s2][c4];
+          x[4 + c4] = (2 * s2 + 1 < KW) ? zr[I][(2 * s2 + 1) % KW][c4] : 0.f;
+        }
+        split3(x, sp[I]);
+      }
+#pragma unroll
+      for (int I = 0; I < NTN; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J) acc[tile_index(I, J)] = mma_split6(sp[I], sp[J], acc[tile_index(I, J)]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < KW; ++j)
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp)
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int J = 0; J <= I; ++J)
+            acc[tile_index(I, J)] = M::mma(zr[I][j][comp], zr[J][j][comp], acc[tile_index(I, J)]);
+  }
+  // kq_e = z_eᵀ Σ_{f∈Q} z_f over this wave's columns (general rows only)
+  if (hasQ) {
+    T gpart[KW][4];
+#pragma unroll
+    for (int j = 0; j < KW; ++j)
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) gpart[j][comp] = T(0);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const bool qe = (mQ >> (16 * I + cl)) & 1;
+#pragma unroll
+      for (int j = 0; j < KW; ++j)
+#pragma unroll
+        for (int comp = 0; comp < 4; ++comp)
+          if (qe) gpart[j][comp] += zr[I][j][comp];
+    }
+#pragma unroll
+    for (int j = 0; j < KW; ++j)
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) gpart[j][comp] = row16_sum(gpart[j][comp]);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      T sq = T(0);
+#pragma unroll
+      for (int j = 0; j < KW; ++j)
+#pragma unroll
+        for (int comp = 0; comp < 4; ++comp) sq += zr[I][j][comp] * gpart[j][comp];
+      sq += shfl_xor(sq, 16);
+      sq += shfl_xor(sq, 32);
+      if (kk == 0) gq[wv][16 * I + cl] = sq;
+    }
+  }
+  // fixed-order reduction of the K partials into wave 0: ((w0 + w2) + (w1 + w3))
+#pragma unroll
+  for (int h = NWK / 2; h >= 1; h /= 2) {
+    if (wv >= h && wv < 2 * h) {
+#pragma unroll
+      for (int t = 0; t < NTT; ++t) red[wv - h][t][lane] = acc[t];
+    }
+    __syncthreads();
+    if (wv < h) {
+#pragma unroll
+      for (int t = 0; t < NTT; ++t) acc[t] += red[wv][t][lane];
+    }
+    __syncthreads();
+  }
+
+  double xb = 0.0;
+  if (wv == 0) {
+    int bad = __any(mine && wl < T(0)) ? 1 : 0;  // negative confidence: not SPD in this form
+    T rhs;
+    if (!hasQ) {
+      // every real signal in P: S = W⁻¹ + K, identity on padding slots
+      const T iw = isP ? fast_rcp(wl) : T(1);
+      rhs = isP ? cwl * iw : T(0);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        const T iwd = __shfl(iw, 16 * I + cl, 64);
+        const int t = tile_index(I, I);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : T(0);
+      }
+    } else {
+      // (W_P⁻¹ + K_PP) u_P = W_P⁻¹ c_P − K_PQ 1_Q,  u_Q = 1
+      rhs = isP ? cwl * fast_rcp(wl) : T(0);
+      if (lane < 16 * NTN) {
+        T kq = T(0);
+#pragma unroll
+        for (int w = 0; w < NWK; ++w) kq += gq[w][lane];
+        if (isP) rhs -= kq;
+      }
+      const T iw = isP ? fast_rcp(wl) : T(0);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        const T iwd = __shfl(iw, 16 * I + cl, 64);
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+          const int f = 16 * J + cl;
+          const bool pf = (mP >> f) & 1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int e = 16 * I + M::crow(lane, r);
+            const bool pe = (mP >> e) & 1;
+            T v = acc[t][r];
+            if (pe && pf) v += (e == f) ? iwd : T(0);
+            else v = (e == f) ? T(1) : T(0);
+            acc[t][r] = v;
+          }
+        }
+      }
+    }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    csync<true>();
+    chol_solve<T, NTN, true>(acc, S, lane, bad);
+    if (!hasQ) {
+      // xᵀb = Σ_e (c_e/w_e)(c_e − u_e)
+      const T ue = lane < 16 * NTN ? S.xs[lane] : T(0);
+      xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
+    }
+    if (lane == 0) sbad = bad;
+  }
+  __syncthreads();
+  // every wave: u of its lane's signals, x' = Zₛᵀu over its columns
+  T ul[NTN], cv[NTN];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int e = 16 * I + cl;
+    const bool pe = (mP >> e) & 1;
+    const bool qe = (mQ >> e) & 1;
+    ul[I] = hasQ ? (pe ? S.xs[e] : (qe ? T(1) : T(0))) : S.xs[e];
+    cv[I] = __shfl(cwl, e, 64);
+  }
+  const bool bad = sbad != 0;
+  double xbw = 0.0;
+#pragma unroll
+  for (int j = 0; j < KW; ++j) {
+    const int q = wv * KW + j;
+    T xq[4];
+#pragma unroll
+    for (int comp = 0; comp < 4; ++comp) {
+      T sx = T(0), sb = T(0);
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        sx += zr[I][j][comp] * ul[I];
+        if (hasQ) sb += zr[I][j][comp] * cv[I];
+      }
+      xq[comp] = row16_sum(sx);
+      if (hasQ) xbw += (double)xq[comp] * (double)row16_sum(sb);
+    }
+    if (q < NTK && cl == j % 16) {
+      v4 o = {xq[0], xq[1], xq[2], xq[3]};
+      if (bad) o = v4{};
+      reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
+    }
+  }
+  if (hasQ) {
+    // xᵀb = x'ᵀ(Zₛᵀc): per-wave partials (one copy per 16-lane row), fixed-order total
+    xbw = wave_sum(cl == 0 ? xbw : 0.0);
+    if (lane == 0) xbp[wv] = xbw;
+    __syncthreads();
+    if (tid == 0) {
+      xb = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWK; ++w) xb += xbp[w];
+    }
+  }
+  if (wv == 0) {
+    const double csum = wave_sum((double)cwl);
+    if (lane == 0) {
+      a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
+      if (bad && a.status) a.status[row] = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Whitening / unwhitening GEMMs with the inverse Cholesky factor Linv = L⁻¹ (lower, KP×KP).
 //   whiten:   Z[r] = Linv · Y[r]     (z = L⁻¹ y)            rows 0..n-1, 16 per wave
 //   unwhiten: X[r] = Linvᵀ · X'[r]   (x = L⁻ᵀ x') in place, rows from `order`; also
@@ -1160,6 +1431,37 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
   return hipGetLastError();
 }
 
+// multi-wave whitened kernel: 4 waves per row
+template <typename T, int NTK>
+static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
+  if (a.nrows <= 0) return hipSuccess;
+  if (!a.desc) return hipErrorInvalidValue;
+  constexpr int NWK = 4;
+#define QMFX_WBMW(N)                                                                   \
+  return launch_row_chunks(a, 64 * NWK, [&](const SolveArgs<T>& c) {                   \
+    hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, N, NWK>), dim3((unsigned)c.nrows), \
+                       dim3(64 * NWK), 0, s, c);                                       \
+  })
+  switch (ntn) {
+    case 1: QMFX_WBMW(1);
+    case 2: QMFX_WBMW(2);
+    case 3:
+      if constexpr (NTK >= 6) QMFX_WBMW(3);
+      return hipErrorInvalidValue;
+    case 4:
+      if constexpr (NTK >= 8) QMFX_WBMW(4);
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+#undef QMFX_WBMW
+}
+
+// the one-wave kernel at fp32 k = 256, or the multi-wave one with QMFX_WB_MW=1
+static bool wb_mw_fp32() {
+  const char* e = std::getenv("QMFX_WB_MW");
+  return e && std::atoi(e) != 0;
+}
+
 template <typename T, int NT>
 static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, int64_t nrows,
                                    const T* Linv, double* rowloss, double lambda, bool unwhiten,
@@ -1320,11 +1622,20 @@ hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s)
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {
+  if (nt == 16 && wb_mw_fp32()) return launch_woodbury_mw_ntk<float, 16>(a, ntn, s);
 #define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, s)
   QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
+  // one wave up to k = 64; k = 80..128 on the multi-wave kernel
+  switch (nt) {
+    case 5: return launch_woodbury_mw_ntk<double, 5>(a, ntn, s);
+    case 6: return launch_woodbury_mw_ntk<double, 6>(a, ntn, s);
+    case 7: return launch_woodbury_mw_ntk<double, 7>(a, ntn, s);
+    case 8: return launch_woodbury_mw_ntk<double, 8>(a, ntn, s);
+    default: break;
+  }
 #define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, s)
   QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
@@ -1340,7 +1651,7 @@ hipError_t launch_whiten(const double* in, double* out, const int64_t* order, in
                          int nt, const double* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s) {
 #define CALL(N) launch_whiten_nt<double, N>(in, out, order, nrows, Linv, rowloss, lambda, unwhiten, s)
-  QMFX_NT_SWITCH64(nt, CALL)
+  QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
 hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
@@ -1352,7 +1663,7 @@ hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* 
 hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
                            int32_t* status, double* scratch, hipStream_t s) {
 #define CALL(N) launch_chol_inv_nt<double, N>(G, k, lambda, Linv, status, scratch, s)
-  QMFX_NT_SWITCH64(nt, CALL)
+  QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
 hipError_t launch_gram(const float* Y, int64_t n, int nt, float* G, double* partial,
