@@ -249,7 +249,18 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 // at most 64 and at most KP/2 (beyond that the k×k solve is the cheaper one).
 // Factor counts beyond one wave's registers (fp32 k > 128, fp64 k > 64) use the multi-wave
 // row kernel and the tiled YᵀY (wals_big.hip).
+// YᵀY on the tiled multi-wave kernel (fp32 k > 128, fp64 k > 64)
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
+// direct rows on the multi-wave row kernel: k > 128.  fp64 k = 80..128 runs the one-wave
+// direct kernel with its accumulators across the VGPR + AGPR file (QMFX_F64_BIG=1 keeps the
+// multi-wave kernel there, for comparisons).
+bool use_big_rows(const qmfx_ctx* c) {
+  if (c->nt > 8) return true;
+  if (c->prec == 32) return false;
+  if (c->nt <= 4) return false;
+  const char* e = std::getenv("QMFX_F64_BIG");
+  return e && std::atoi(e) != 0;
+}
 
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
@@ -838,7 +849,8 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            (const double*)c->Linv, nullptr, 0.0, false, c->stream));
     }
   }
-  if (!big) {
+  const bool big_rows = use_big_rows(c);
+  if (!big_rows) {
     if (fp32)
       HIPCHK(launch_gimg((const float*)c->G, c->nt, c->k, lambda, (float*)c->Gimg, c->stream));
     else
@@ -870,13 +882,15 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            d0, nd, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc,
                            (const float*)c->Gimg, trace_path ? c->trace : nullptr,
                            (int32_t)R.n};
-        HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
+        HIPCHK(big_rows ? launch_wals_big(a, c->nt, c->stream)
+                        : launch_wals_direct(a, c->nt, c->stream));
       } else {
         SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)R.F,
                             (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
                             d0, nd, alpha, lambda, c->k, c->ablate, L.d_desc,
                             (const double*)c->Gimg, nullptr, (int32_t)R.n};
-        HIPCHK(big ? launch_wals_big(a, c->nt, c->stream) : launch_wals_direct(a, c->nt, c->stream));
+        HIPCHK(big_rows ? launch_wals_big(a, c->nt, c->stream)
+                        : launch_wals_direct(a, c->nt, c->stream));
       }
     }
     HIPCHK(hipEventRecord(c->evp[j][1], c->stream));

@@ -468,8 +468,15 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_WAVES_NT8
 #define QMFX_WAVES_NT8 1
 #endif
+// waves per SIMD the direct kernel is compiled for: fp32 split-Gram and fp64 k > 64 tilings
+// keep their accumulators in the whole (VGPR + AGPR) register file of one wave
+template <typename T, int NT>
+constexpr int direct_waves() {
+  return Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : (sizeof(T) == 8 && NT > 4 ? 1 : 2);
+}
+
 template <typename T, int NT, bool TRACE>
-__global__ __launch_bounds__(64, Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : 2)
+__global__ __launch_bounds__(64, (direct_waves<T, NT>()))
 void wals_direct_kernel(SolveArgs<T> a) {
   // fp32 at NT = 8: the split-bf16 Gram keeps 144 accumulator + 96 operand + 128 row
   // registers live: one wave per SIMD with the whole register file (QMFX_WAVES_NT8 = 1)
@@ -1608,7 +1615,7 @@ hipError_t launch_gimg(const float* G, int nt, int k, double lambda, float* img,
 hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* img,
                        hipStream_t s) {
 #define CALL(N) launch_gimg_nt<double, N>(G, k, lambda, img, s)
-  QMFX_NT_SWITCH64(nt, CALL)
+  QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s) {
@@ -1618,7 +1625,7 @@ hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s) 
 }
 hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s) {
 #define CALL(N) launch_direct_nt<double, N>(a, s)
-  QMFX_NT_SWITCH64(nt, CALL)
+  QMFX_NT_SWITCH(nt, CALL)
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {

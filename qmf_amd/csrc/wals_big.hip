@@ -10,9 +10,9 @@
 //     buffer, register-staged loads of the next stage in flight during the MFMAs); every
 //     wave reads its tiles' operands from LDS, so the tile→wave map is a runtime table;
 //   * Cholesky, right-looking over 16-column panels: owners write panel column p to LDS,
-//     wave 0 factors it (streamed 64 rows at a time: register cost independent of k) and
-//     forward-solves b, then every wave applies the rank-16 trailing update to its own
-//     tiles with MFMA (operands from the LDS panel) — three barriers per panel;
+//     wave 0 factors its diagonal block and the next 48 rows, the waves solve the remaining
+//     rows 64 at a time in parallel (with the forward solve of b), then every wave applies
+//     the rank-16 trailing update to its own tiles with MFMA (operands from the LDS panel);
 //   * backward solve by 16-blocks: owners of L(J, I) tiles add their part of Lᵀx in LDS,
 //     wave 0 finishes the block with the diagonal triangle.
 // Same results contract as the single-wave kernels: status[row] = 1 on a non-positive pivot.
@@ -26,6 +26,13 @@
 #include "kernels.h"
 #include "rowsolve.h"
 
+#ifndef QMFX_BIG_SIG32
+#define QMFX_BIG_SIG32 32
+#endif
+#ifndef QMFX_BIG_SIG64
+#define QMFX_BIG_SIG64 16
+#endif
+
 namespace qmfx {
 
 template <typename T, int NT>
@@ -36,7 +43,7 @@ struct BigCfg {
   static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : 8) : (NT <= 8 ? 4 : 8);
   static constexpr int TPW = (NTT + NW - 1) / NW;
   static constexpr int NTHR = 64 * NW;
-  static constexpr int SIG = sizeof(T) == 4 ? 32 : 16;  // signals per LDS stage
+  static constexpr int SIG = sizeof(T) == 4 ? QMFX_BIG_SIG32 : QMFX_BIG_SIG64;  // signals per LDS stage
   static constexpr int VEC = 16 / sizeof(T);             // elements per 16-B load
   static constexpr int CPR = KP / VEC;                   // 16-B chunks per row
   static constexpr int TRIPS = (SIG * CPR + NTHR - 1) / NTHR;
@@ -63,74 +70,75 @@ struct BigShared {
   int bad;  // wave 0's pivot flag, for every wave's output stores
 };
 
-// Panel p of the right-looking Cholesky, by ONE wave: rows 16p..KP-1 of column block p are
-// in S.panel (row q at q·PLD), the right-hand side in S.bw.  Factors the 16×16 diagonal
-// block (L, 1/diag in S.invd), solves the rows below against it, applies the forward
-// substitution to b, writes L back to S.panel and the diagonal block to S.Ldiag.
-// Rows are processed 64 per slot; slot 0 holds the diagonal block.
+// Panel p of the right-looking Cholesky.  Rows 16p..KP-1 of column block p are in S.panel
+// (row q at q·PLD), the right-hand side in S.bw.  Head (one wave): rows 0..63 of the panel —
+// factors the 16×16 diagonal block (L, 1/diag in S.invd), solves the 48 rows below it,
+// applies the forward substitution to b and keeps the diagonal block in S.Ldiag.
 template <typename T, int NT>
-__device__ void big_panel(BigShared<T, NT>& S, int p, int lane, int& bad) {
+__device__ void big_panel_head(BigShared<T, NT>& S, int p, int lane, int& bad) {
   constexpr int KP = 16 * NT;
   constexpr int PLD = BigCfg<T, NT>::PLD;
   const int R = KP - 16 * p;
-  const int cl = lane & 15;
-  // slot 0: rows 0..63 (diagonal block + up to 48 rows below)
-  {
-    const int q = lane;
-    const bool live = q < R;
-    T pa[16];
+  const int q = lane;
+  const bool live = q < R;
+  T pa[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
-    T pb = live ? S.bw[16 * p + q] : T(0);
+  for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
+  T pb = live ? S.bw[16 * p + q] : T(0);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const T d = readlane(pa[c], c);
-      bad |= !(d > T(0));
-      const T ljj = fast_sqrt(d);
-      const T inv = fast_rcp(ljj);
-      if (lane == 0) S.invd[16 * p + c] = inv;
-      const T lq = q > c ? pa[c] * inv : T(0);
-      pa[c] = q > c ? lq : (q == c ? ljj : pa[c]);
-      const T yc = readlane(pb, c) * inv;
-      if (lane == 0) S.bw[16 * p + c] = yc;
-      pb -= lq * yc;
+  for (int c = 0; c < 16; ++c) {
+    const T d = readlane(pa[c], c);
+    bad |= !(d > T(0));
+    const T ljj = fast_sqrt(d);
+    const T inv = fast_rcp(ljj);
+    if (lane == 0) S.invd[16 * p + c] = inv;
+    const T lq = q > c ? pa[c] * inv : T(0);
+    pa[c] = q > c ? lq : (q == c ? ljj : pa[c]);
+    const T yc = readlane(pb, c) * inv;
+    if (lane == 0) S.bw[16 * p + c] = yc;
+    pb -= lq * yc;
 #pragma unroll
-      for (int m = c + 1; m < 16; ++m) pa[m] -= lq * readlane(lq, m);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (live) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
-      if (q >= 16) S.bw[16 * p + q] = pb;
-    }
-    for (int idx = lane; idx < 256; idx += 64) {
-      const int r = idx >> 4, c = idx & 15;
-      S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
-    }
+    for (int m = c + 1; m < 16; ++m) pa[m] -= lq * readlane(lq, m);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  // further slots: L(q, :) = A(q, :) · L_diag⁻ᵀ column by column, and b(q) -= L(q, c)·y_c
-  for (int base = 64; base < R; base += 64) {
-    const int q = base + lane;
-    const bool live = q < R;
-    T pa[16];
+  if (live) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
-    T pb = live ? S.bw[16 * p + q] : T(0);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const T lq = pa[c] * S.invd[16 * p + c];
-      pa[c] = lq;
-      pb -= lq * S.bw[16 * p + c];
-#pragma unroll
-      for (int m = c + 1; m < 16; ++m) pa[m] -= lq * S.Ldiag[(p * 16 + m) * PLD + c];
-    }
-    if (live) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
-      S.bw[16 * p + q] = pb;
-    }
+    for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
+    if (q >= 16) S.bw[16 * p + q] = pb;
   }
-  (void)cl;
+  for (int idx = lane; idx < 256; idx += 64) {
+    const int r = idx >> 4, c = idx & 15;
+    S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
+  }
+}
+
+// Rows base..base+63 of panel p (base ≥ 64), after the head: L(q, :) = A(q, :) · L_diag⁻ᵀ
+// column by column and b(q) −= L(q, c)·y_c.  Independent rows: the slots of a panel run on
+// different waves at once.
+template <typename T, int NT>
+__device__ void big_panel_slot(BigShared<T, NT>& S, int p, int base, int lane) {
+  constexpr int KP = 16 * NT;
+  constexpr int PLD = BigCfg<T, NT>::PLD;
+  const int R = KP - 16 * p;
+  const int q = base + lane;
+  const bool live = q < R;
+  T pa[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
+  T pb = live ? S.bw[16 * p + q] : T(0);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const T lq = pa[c] * S.invd[16 * p + c];
+    pa[c] = lq;
+    pb -= lq * S.bw[16 * p + c];
+#pragma unroll
+    for (int m = c + 1; m < 16; ++m) pa[m] -= lq * S.Ldiag[(p * 16 + m) * PLD + c];
+  }
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
+    S.bw[16 * p + q] = pb;
+  }
 }
 
 // One 4-signal step of the Gram for the tiles of wave W (t = W + NW·s, compile-time map):
@@ -352,7 +360,14 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       }
     }
     __syncthreads();
-    if (wv == 0 && !(a.ablate & 2)) big_panel<T, NT>(S, p, lane, bad);
+    if (!(a.ablate & 2)) {
+      if (wv == 0) big_panel_head<T, NT>(S, p, lane, bad);
+      if (KP - 16 * p > 64) {
+        __syncthreads();
+        for (int base = 64 * (1 + wv); base < KP - 16 * p; base += 64 * NW)
+          big_panel_slot<T, NT>(S, p, base, lane);
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {
