@@ -920,6 +920,12 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 // wave 0, which solves the n×n system alone (chol_solve with wave-local LDS ordering); u
 // goes back through LDS and every wave forms x' = Zₛᵀu for its own columns.
 // ---------------------------------------------------------------------------------------
+#ifndef QMFX_MW_NWK
+// waves per row of the multi-wave whitened kernel (2 beats 4 at fp64 k = 128, 421 -> 314 ms
+// per C3 user half, and the one-wave kernel at fp32 k = 256, 193 -> 167 ms per C5 user half:
+// twice the rows in flight per CU, one idle wave during the n×n solve instead of three)
+#define QMFX_MW_NWK 2
+#endif
 template <typename T, int NTK, int NTN, int NWK>
 struct MwCfg {
   static constexpr int KW = (NTK + NWK - 1) / NWK;  // column blocks of 16 per wave
@@ -935,7 +941,7 @@ __global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs
   constexpr int KP = 16 * NTK;
   constexpr int KW = C::KW;
   constexpr int NTT = C::NTT;
-  static_assert(NWK == 2 || NWK == 4, "wave count");
+  static_assert(NWK == 2 || NWK == 4, "wave count");  // the K reduction tree
   __shared__ __attribute__((aligned(16))) CholShared<T, NTN> S;
   __shared__ __attribute__((aligned(16))) acc_t red[NWK / 2][NTT][64];
   __shared__ T gq[NWK][16 * NTN];
@@ -1443,7 +1449,7 @@ template <typename T, int NTK>
 static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
-  constexpr int NWK = 4;
+  constexpr int NWK = QMFX_MW_NWK;
 #define QMFX_WBMW(N)                                                                   \
   return launch_row_chunks(a, 64 * NWK, [&](const SolveArgs<T>& c) {                   \
     hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, N, NWK>), dim3((unsigned)c.nrows), \
@@ -1463,10 +1469,10 @@ static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStre
 #undef QMFX_WBMW
 }
 
-// the one-wave kernel at fp32 k = 256, or the multi-wave one with QMFX_WB_MW=1
+// fp32 k = 256: the multi-wave kernel, or the one-wave one with QMFX_WB_MW=0
 static bool wb_mw_fp32() {
   const char* e = std::getenv("QMFX_WB_MW");
-  return e && std::atoi(e) != 0;
+  return !e || std::atoi(e) != 0;
 }
 
 template <typename T, int NT>
