@@ -202,7 +202,9 @@ def parity_check(ctx, cfg, nthreads, nsample=1000):
 CLASS_KERNELS = {
     "wals_direct_kernel": ("wals_direct_kernel<",),
     "wals_big_kernel": ("wals_big_kernel<",),
-    "wals_whitened (row solve + unwhiten)": ("wals_woodbury_kernel<", "whiten_kernel<{T}, {NT}, true>"),
+    "wals_whitened (row solve + unwhiten)": ("wals_woodbury_kernel<", "wals_woodbury_mw_kernel<",
+                                             "whiten_kernel<{T}, {NT}, true>"),
+    "bpr_epoch_kernel": ("bpr_epoch_kernel<",),
 }
 
 
@@ -297,10 +299,14 @@ def bench_bpr(args, rank, world):
                    % (args.config, nu, ni, nnz, num_neg, k)},
         "roofline": {"kernel": "bpr_epoch_kernel", "bound": "hbm",
                      "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                     "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 4),
                      "launch_ms": round(sec * 1e3, 3)},
         "eval_loss": loss,
     }
+    traffic, tsrc = pmc_traffic(args.config, args.precision, "bpr_epoch_kernel", k)
+    out["roofline"].update({"traffic": round(traffic, 0) if traffic else None,
+                            "traffic_algorithmic_ratio": round(traffic / by, 3) if traffic else None,
+                            "traffic_source": tsrc})
     if args.cpu_baseline != "none" and rank == 0:
         # one full reference-structure Hogwild epoch (BPREngine::optimize with
         # numHogwildThreads = nthreads) + its evaluation pass, from the device's factors
@@ -397,7 +403,8 @@ def main():
     peak_tf = PEAK_F32_TFLOPS if args.precision == 32 else PEAK_F64_TFLOPS
     ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
     classes = {}
-    direct_name = "wals_big_kernel" if (k > 128 if args.precision == 32 else k > 64) else "wals_direct_kernel"
+    # direct rows: the one-wave kernel up to k = 128 (fp32 and fp64), the multi-wave one above
+    direct_name = "wals_big_kernel" if k > 128 else "wals_direct_kernel"
     for cls, name in ((0, direct_name), (1, "wals_whitened (row solve + unwhiten)")):
         ks = ctx.kernel_stats(cls)
         if ks["launches"] == 0 or ks["ms"] <= 0:

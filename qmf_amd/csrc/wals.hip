@@ -378,8 +378,13 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   auto load_rows = [&](const int (&col)[8], vecW (&y)[8][NG]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+#ifdef QMFX_EXP_LOCAL_GATHER  // timing experiment: every gather hits a few cached rows
+      const vecW* yr =
+          reinterpret_cast<const vecW*>(a.Y + (uint64_t)(uint32_t)(col[j] & 63) * KP) + c;
+#else
       const vecW* yr =
           reinterpret_cast<const vecW*>(a.Y + (uint64_t)(uint32_t)col[j] * KP) + c;
+#endif
 #pragma unroll
       for (int G = 0; G < NG; ++G) y[j][G] = yr[16 * G];
     }
