@@ -154,12 +154,21 @@ def cpu_epoch(ctx, cfg, nthreads):
     o.set_factors(1, ctx.factors(1))
     t_build = time.perf_counter() - t0
     log("cpu epoch: oracle built in %.1fs; running one epoch on %d threads" % (t_build, nthreads))
+    import threading
+    done = threading.Event()
+
+    def heartbeat():  # the port runs minutes inside one ctypes call (GIL released)
+        while not done.wait(30.0):
+            log("cpu epoch: running, %.0fs" % (time.perf_counter() - t1))
     t1 = time.perf_counter()
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
     o.iterate(0, nthreads)
     t_u = time.perf_counter() - t1
     log("cpu epoch: user half %.1fs" % t_u)
     loss = o.iterate(1, nthreads)
     t = time.perf_counter() - t1
+    done.set()
     return t, {"lapack": lapack, "t_user_half": round(t_u, 3), "t_item_half": round(t - t_u, 3),
                "t_build": round(t_build, 3), "loss": loss}
 
