@@ -47,4 +47,27 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
+template <int CTL>
+__device__ __forceinline__ float dpp_mov_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTL, 0xf, 0xf, false));
+}
+// Four independent 16-lane row sums in lockstep: each DPP step reads a value written three
+// instructions earlier, so no hazard padding (s_nop) separates the steps of one chain.
+template <int CTL, typename T>
+__device__ __forceinline__ T dpp_step(T v) {
+  if constexpr (sizeof(T) == 4) return dpp_mov_f32<CTL>(v);
+  else return dpp_mov_f64<CTL>(v);
+}
+template <typename T>
+__device__ __forceinline__ void row16_sum4(T (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += dpp_step<0x128>(v[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += dpp_step<0x124>(v[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += dpp_step<0x122>(v[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += dpp_step<0x121>(v[i]);
+}
+
 }  // namespace qmfx

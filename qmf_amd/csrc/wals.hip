@@ -98,6 +98,11 @@ __device__ __forceinline__ f32x4 mma_split6(const Split3& a, const Split3& b, f3
 // LDS transposed and column-scaled, Lt[q][c] = L[c][q]/L[q][q] (q < c, 0 elsewhere), so
 // the backward substitution is one readlane + one FMA per column.
 // ---------------------------------------------------------------------------------------
+#ifndef QMFX_CHOL_PK
+#define QMFX_CHOL_PK 1
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <typename T>
 struct CholLd {
   // padded LDS row of a panel: fp32 rows are 16-B aligned and conflict-free for the
@@ -215,9 +220,28 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
             const T lqs = lq * inv;
             pa[s][c] = lq;
             pb[s] -= lqs * bc;
+#if QMFX_CHOL_PK
+            if constexpr (sizeof(T) == 4) {
+              // packed pairs: one v_pk_fma_f32 per two columns (same rounding as two FMAs)
 #pragma unroll
-            for (int m = 1; m < 16; ++m)
-              if (m > c) pa[s][m] -= lqs * am[m];
+              for (int m = 0; m < 16; m += 2) {
+                if (m > c) {
+                  f32x2 v = {pa[s][m], pa[s][m + 1]};
+                  const f32x2 a2 = {am[m], am[m + 1]};
+                  v = __builtin_elementwise_fma(f32x2{-lqs, -lqs}, a2, v);
+                  pa[s][m] = v[0];
+                  pa[s][m + 1] = v[1];
+                } else if (m + 1 > c) {
+                  pa[s][m + 1] -= lqs * am[m + 1];
+                }
+              }
+            } else
+#endif
+            {
+#pragma unroll
+              for (int m = 1; m < 16; ++m)
+                if (m > c) pa[s][m] -= lqs * am[m];
+            }
           }
         }
         // one column per scheduling window: readlanes hoisted across columns exhaust the
@@ -805,9 +829,7 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
             if (qe) gpart[q][comp] += zr[I][q][comp];
       }
 #pragma unroll
-      for (int q = 0; q < NTK; ++q)
-#pragma unroll
-        for (int comp = 0; comp < 4; ++comp) gpart[q][comp] = row16_sum(gpart[q][comp]);
+      for (int q = 0; q < NTK; ++q) row16_sum4(gpart[q]);
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
         T sq = T(0);
@@ -864,16 +886,21 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
     // xᵀb = x'ᵀ(Zₛᵀc)
 #pragma unroll
     for (int q = 0; q < NTK; ++q) {
+      T sx[4], sb[4];
 #pragma unroll
       for (int comp = 0; comp < 4; ++comp) {
-        T sx = T(0), sb = T(0);
+        sx[comp] = T(0);
+        sb[comp] = T(0);
 #pragma unroll
         for (int I = 0; I < NTN; ++I) {
-          sx += zr[I][q][comp] * ul[I];
-          sb += zr[I][q][comp] * cv[I];
+          sx[comp] += zr[I][q][comp] * ul[I];
+          sb[comp] += zr[I][q][comp] * cv[I];
         }
-        xb += (double)row16_sum(sx) * (double)row16_sum(sb);
       }
+      row16_sum4(sx);
+      row16_sum4(sb);
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) xb += (double)sx[comp] * (double)sb[comp];
     }
     xb = wave_sum(cl == 0 ? xb : 0.0);
   }
@@ -888,8 +915,9 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
       T sx = T(0);
 #pragma unroll
       for (int I = 0; I < NTN; ++I) sx += zr[I][q][comp] * ul[I];
-      xq[comp] = row16_sum(sx);
+      xq[comp] = sx;
     }
+    row16_sum4(xq);
     if (cl == q) {
       v4 o = {xq[0], xq[1], xq[2], xq[3]};
       if (bad) o = v4{};
@@ -925,6 +953,9 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 // wave 0, which solves the n×n system alone (chol_solve with wave-local LDS ordering); u
 // goes back through LDS and every wave forms x' = Zₛᵀu for its own columns.
 // ---------------------------------------------------------------------------------------
+#ifndef QMFX_MW_F64_NTN4_DEFAULT
+#define QMFX_MW_F64_NTN4_DEFAULT 2
+#endif
 #ifndef QMFX_MW_NWK
 // waves per row of the multi-wave whitened kernel (2 beats 4 at fp64 k = 128, 421 -> 314 ms
 // per C3 user half, and the one-wave kernel at fp32 k = 256, 193 -> 167 ms per C5 user half:
@@ -1039,9 +1070,7 @@ __global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs
           if (qe) gpart[j][comp] += zr[I][j][comp];
     }
 #pragma unroll
-    for (int j = 0; j < KW; ++j)
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp) gpart[j][comp] = row16_sum(gpart[j][comp]);
+    for (int j = 0; j < KW; ++j) row16_sum4(gpart[j]);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       T sq = T(0);
@@ -1140,17 +1169,22 @@ __global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs
 #pragma unroll
   for (int j = 0; j < KW; ++j) {
     const int q = wv * KW + j;
-    T xq[4];
+    T xq[4], sb[4];
 #pragma unroll
     for (int comp = 0; comp < 4; ++comp) {
-      T sx = T(0), sb = T(0);
+      xq[comp] = T(0);
+      sb[comp] = T(0);
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
-        sx += zr[I][j][comp] * ul[I];
-        if (hasQ) sb += zr[I][j][comp] * cv[I];
+        xq[comp] += zr[I][j][comp] * ul[I];
+        if (hasQ) sb[comp] += zr[I][j][comp] * cv[I];
       }
-      xq[comp] = row16_sum(sx);
-      if (hasQ) xbw += (double)xq[comp] * (double)row16_sum(sb);
+    }
+    row16_sum4(xq);
+    if (hasQ) {
+      row16_sum4(sb);
+#pragma unroll
+      for (int comp = 0; comp < 4; ++comp) xbw += (double)xq[comp] * (double)sb[comp];
     }
     if (q < NTK && cl == j % 16) {
       v4 o = {xq[0], xq[1], xq[2], xq[3]};
@@ -1398,8 +1432,9 @@ __global__ void mfma_selftest_kernel(const T* A, const T* B, T* C) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Host launchers.
+// Host launchers.  (QMFX_KERNELS_ONLY: kernel-only builds for ISA inspection, tools/isa_one.sh)
 // ---------------------------------------------------------------------------------------
+#ifndef QMFX_KERNELS_ONLY
 template <typename T, int NT>
 static hipError_t launch_direct_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
@@ -1450,11 +1485,25 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
 }
 
 // multi-wave whitened kernel: 4 waves per row
+// fp64 n×n bucket 4 at k = 128: 2 waves per row spill 76 VGPRs, 4 waves do not
+// (QMFX_MW_F64_NTN4 = 2 or 4 picks one for comparisons)
+static int mw_f64_ntn4_waves() {
+  const char* e = std::getenv("QMFX_MW_F64_NTN4");
+  return e ? std::atoi(e) : QMFX_MW_F64_NTN4_DEFAULT;
+}
+
 template <typename T, int NTK>
 static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   constexpr int NWK = QMFX_MW_NWK;
+  if constexpr (sizeof(T) == 8 && NTK >= 8) {
+    if (ntn == 4 && mw_f64_ntn4_waves() == 4)
+      return launch_row_chunks(a, 256, [&](const SolveArgs<T>& c) {
+        hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, 4, 4>), dim3((unsigned)c.nrows),
+                           dim3(256), 0, s, c);
+      });
+  }
 #define QMFX_WBMW(N)                                                                   \
   return launch_row_chunks(a, 64 * NWK, [&](const SolveArgs<T>& c) {                   \
     hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, N, NWK>), dim3((unsigned)c.nrows), \
@@ -1713,5 +1762,6 @@ hipError_t launch_mfma_selftest_f64(const double* A, const double* B, double* C,
   hipLaunchKernelGGL(mfma_selftest_kernel<double>, dim3(1), dim3(64), 0, s, A, B, C);
   return hipGetLastError();
 }
+#endif  // QMFX_KERNELS_ONLY
 
 }  // namespace qmfx
