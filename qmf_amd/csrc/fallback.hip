@@ -235,6 +235,24 @@ __global__ __launch_bounds__(FB_THREADS) void wals_system_kernel(FallbackArgs<T>
   if (tid == 0) out[(size_t)k * k + k] = csum;
 }
 
+// End-of-half status in one block for one async copy to pinned host memory: the loss sum,
+// the re-solved and singular row counts, and the YᵀY + λI factorization flag.
+__global__ void half_status_kernel(const double* loss, const unsigned long long* fb,
+                                   const int32_t* chol, double* out) {
+  if (threadIdx.x == 0) {
+    out[0] = loss[0];
+    out[1] = (double)fb[0];
+    out[2] = (double)fb[1];
+    out[3] = chol ? (double)chol[0] : 0.0;
+  }
+}
+
+hipError_t launch_half_status(const double* loss, const unsigned long long* fb,
+                              const int32_t* chol, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(half_status_kernel, dim3(1), dim3(64), 0, s, loss, fb, chol, out);
+  return hipGetLastError();
+}
+
 int fallback_grid(int64_t nslots) {
   const int64_t g = (nslots + 4095) / 4096;
   return (int)(g < 1 ? 1 : (g > FB_MAX_GRID ? FB_MAX_GRID : g));

@@ -121,6 +121,10 @@ hipError_t launch_wals_system(const FallbackArgs<float>& a, int64_t beg, int64_t
 hipError_t launch_wals_system(const FallbackArgs<double>& a, int64_t beg, int64_t end,
                               double* out, hipStream_t s);
 
+// out[0] = *loss, out[1..2] = fb[0..1], out[3] = *chol (0 when chol is null)
+hipError_t launch_half_status(const double* loss, const unsigned long long* fb,
+                              const int32_t* chol, double* out, hipStream_t s);
+
 // BPR (bpr.hip)
 template <typename T>
 struct BprArgs {

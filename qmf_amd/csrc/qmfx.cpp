@@ -41,6 +41,7 @@ int fail(const std::string& m, int code = -1) {
   } while (0)
 
 #define QMFX_MAX_PIECES 16
+constexpr int kHalfStatus = 1024;  // dsum offset of the end-of-half status block
 
 struct SideBuf {
   int64_t n = 0;
@@ -461,7 +462,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (e == hipSuccess) e = hipMalloc(&c->G, (size_t)c->kp * c->kp * c->esz);
   if (e == hipSuccess)
     e = hipMalloc(&c->gpart, (size_t)c->gpart_blocks * (nt * (nt + 1) / 2) * 256 * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc(&c->dsum, 1024 * sizeof(double));  // sum + partials
+  // sum + partials (launch_sum_f64: 1 + kSumBlocks), then the half status block
+  if (e == hipSuccess) e = hipMalloc(&c->dsum, (kHalfStatus + 4) * sizeof(double));
   if (e == hipSuccess) e = hipHostMalloc(&c->hsum, 4 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc(&c->bad, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->eval_partial, 1024 * sizeof(double));
@@ -963,16 +965,17 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
   }
   HIPCHK(hipEventRecord(c->evh[2], c->stream));
-  HIPCHK(hipMemcpyAsync(c->hsum, c->dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  unsigned long long fb[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(fb, c->fb_cnt, sizeof(fb), hipMemcpyDeviceToHost, c->stream));
+  // loss, re-solve counts and the factorization flag: one small copy into pinned memory
+  HIPCHK(launch_half_status(c->dsum, c->fb_cnt, use_w ? c->chol_status : nullptr,
+                            c->dsum + kHalfStatus, c->stream));
+  HIPCHK(hipMemcpyAsync(c->hsum, c->dsum + kHalfStatus, 4 * sizeof(double),
+                        hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  c->fb_rows = (int64_t)fb[0];
+  c->fb_rows = (int64_t)c->hsum[1];
   // the reference's CHECK(info == 0) after dsysv_ (Matrix.cpp:94)
-  if (fb[1]) return fail(std::to_string(fb[1]) + " singular row system(s) (dsysv info > 0)", -6);
-  int32_t chol_bad = 0;
-  if (use_w) HIPCHK(hipMemcpy(&chol_bad, c->chol_status, 4, hipMemcpyDeviceToHost));
-  if (chol_bad) return fail("YᵀY + λI is not positive definite", -5);
+  if (c->hsum[2] != 0.0)
+    return fail(std::to_string((int64_t)c->hsum[2]) + " singular row system(s) (dsysv info > 0)", -6);
+  if (c->hsum[3] != 0.0) return fail("YᵀY + λI is not positive definite", -5);
   // timing and algorithmic work per kernel class (SURVEY.md §8(d) accounting)
   float ms_d = 0.f, ms_w = 0.f, ms_h = 0.f;
   for (int j = 0; j < P; ++j) {

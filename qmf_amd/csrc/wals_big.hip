@@ -29,6 +29,9 @@
 #ifndef QMFX_BIG_SIG32
 #define QMFX_BIG_SIG32 32
 #endif
+#ifndef QMFX_BIG_NW32
+#define QMFX_BIG_NW32 8  // waves per row at fp32 k > 160
+#endif
 #ifndef QMFX_BIG_SIG64
 #define QMFX_BIG_SIG64 16
 #endif
@@ -40,7 +43,7 @@ struct BigCfg {
   static constexpr int KP = 16 * NT;
   static constexpr int NTT = NT * (NT + 1) / 2;
   // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave
-  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : 8) : (NT <= 8 ? 4 : 8);
+  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? 4 : 8);
   static constexpr int TPW = (NTT + NW - 1) / NW;
   static constexpr int NTHR = 64 * NW;
   static constexpr int SIG = sizeof(T) == 4 ? QMFX_BIG_SIG32 : QMFX_BIG_SIG64;  // signals per LDS stage
@@ -69,6 +72,17 @@ struct BigShared {
   double red[C::NW];
   int bad;  // wave 0's pivot flag, for every wave's output stores
 };
+
+// Calls f(integral_constant<W>) for the wave-uniform wave index wv (compile-time tile maps).
+template <int NW, int W = 0, typename F>
+__device__ __forceinline__ void dispatch_wave(int wv, F&& f) {
+  if constexpr (W < NW) {
+    if (wv == W)
+      f(std::integral_constant<int, W>{});
+    else
+      dispatch_wave<NW, W + 1>(wv, f);
+  }
+}
 
 // Panel p of the right-looking Cholesky.  Rows 16p..KP-1 of column block p are in S.panel
 // (row q at q·PLD), the right-hand side in S.bw.  Head (one wave): rows 0..63 of the panel —
@@ -305,18 +319,9 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
         for (int k4 = 0; k4 < SIG; k4 += 4)
           big_gram_step<T, NT, W>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk]);
       };
-      static_assert(NW == 4 || NW == 8, "wave count");
+      static_assert(NW == 4 || NW == 8 || NW == 16, "wave count");
       if constexpr (C::REUSE) {
-        switch (wv) {
-          case 0: gram_stage(std::integral_constant<int, 0>{}); break;
-          case 1: gram_stage(std::integral_constant<int, 1>{}); break;
-          case 2: gram_stage(std::integral_constant<int, 2>{}); break;
-          case 3: gram_stage(std::integral_constant<int, 3>{}); break;
-          case 4: gram_stage(std::integral_constant<int, 4 % NW>{}); break;
-          case 5: gram_stage(std::integral_constant<int, 5 % NW>{}); break;
-          case 6: gram_stage(std::integral_constant<int, 6 % NW>{}); break;
-          default: gram_stage(std::integral_constant<int, 7 % NW>{}); break;
-        }
+        dispatch_wave<NW>(wv, gram_stage);
       } else {
 #pragma unroll 2
         for (int k4 = 0; k4 < SIG; k4 += 4) {
@@ -391,16 +396,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       auto trailing = [&](auto wtag) {
         big_trailing<T, NT, decltype(wtag)::value>(acc, S.panel, p, cl, kk);
       };
-      switch (wv) {
-        case 0: trailing(std::integral_constant<int, 0>{}); break;
-        case 1: trailing(std::integral_constant<int, 1>{}); break;
-        case 2: trailing(std::integral_constant<int, 2>{}); break;
-        case 3: trailing(std::integral_constant<int, 3>{}); break;
-        case 4: trailing(std::integral_constant<int, 4 % NW>{}); break;
-        case 5: trailing(std::integral_constant<int, 5 % NW>{}); break;
-        case 6: trailing(std::integral_constant<int, 6 % NW>{}); break;
-        default: trailing(std::integral_constant<int, 7 % NW>{}); break;
-      }
+      dispatch_wave<NW>(wv, trailing);
     }
     __syncthreads();
   }
@@ -512,16 +508,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void gram_tiles_kernel(
         for (int k4 = 0; k4 < SIG; k4 += 4)
           big_gram_step<T, NT, decltype(wtag)::value>(acc, stage + (k4 + kk) * KP + cl, T(1));
       };
-      switch (wv) {
-        case 0: step(std::integral_constant<int, 0>{}); break;
-        case 1: step(std::integral_constant<int, 1>{}); break;
-        case 2: step(std::integral_constant<int, 2>{}); break;
-        case 3: step(std::integral_constant<int, 3>{}); break;
-        case 4: step(std::integral_constant<int, 4 % NW>{}); break;
-        case 5: step(std::integral_constant<int, 5 % NW>{}); break;
-        case 6: step(std::integral_constant<int, 6 % NW>{}); break;
-        default: step(std::integral_constant<int, 7 % NW>{}); break;
-      }
+      dispatch_wave<NW>(wv, step);
     } else {
       for (int k4 = 0; k4 < SIG; k4 += 4) {
         const T* yk = stage + (k4 + kk) * KP + cl;
@@ -542,20 +529,31 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void gram_tiles_kernel(
   }
 }
 
-// fixed-order fp64 sum of the per-block partials + mirror (runtime NT)
+// fixed-order fp64 sum of the per-block partials + mirror (runtime NT): 16 outputs per
+// block, 16 chunk sums each, then the chunks in order (as gram_reduce_kernel in wals.hip)
 template <typename T>
-__global__ void gram_reduce_rt_kernel(const double* partial, int nblocks, int nt, T* G) {
+__global__ __launch_bounds__(256) void gram_reduce_rt_kernel(const double* partial, int nblocks,
+                                                             int nt, T* G) {
+  __shared__ double red[16][16];
   const int KP = 16 * nt;
   const int NTT = nt * (nt + 1) / 2;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= KP * KP) return;
+  const int o = threadIdx.x & 15, ch = threadIdx.x >> 4;
+  const int idx = blockIdx.x * 16 + o;
   const int i = idx / KP, j = idx % KP;
   const int ii = i >= j ? i : j, jj = i >= j ? j : i;
   const int t = tile_index(ii >> 4, jj >> 4);
   const int off = t * 256 + (ii & 15) * 16 + (jj & 15);
+  const int cs = (nblocks + 15) / 16;
+  const int b0 = ch * cs, b1 = b0 + cs < nblocks ? b0 + cs : nblocks;
   double sum = 0.0;
-  for (int b = 0; b < nblocks; ++b) sum += partial[(int64_t)b * NTT * 256 + off];
-  G[idx] = (T)sum;
+  for (int b = b0; b < b1; ++b) sum += partial[(int64_t)b * NTT * 256 + off];
+  red[ch][o] = sum;
+  __syncthreads();
+  if (ch == 0) {
+    double tot = 0.0;
+    for (int c = 0; c < 16; ++c) tot += red[c][o];
+    G[idx] = (T)tot;
+  }
 }
 
 template <typename T, int NT>
@@ -616,7 +614,7 @@ static hipError_t gram_big(const T* Y, int64_t n, int nt, T* G, double* partial,
 #undef CALL
   if (e != hipSuccess) return e;
   const int KP = 16 * nt;
-  hipLaunchKernelGGL((gram_reduce_rt_kernel<T>), dim3((KP * KP + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL((gram_reduce_rt_kernel<T>), dim3(KP * KP / 16), dim3(256), 0, s,
                      partial, nblocks, nt, G);
   return hipGetLastError();
 }
