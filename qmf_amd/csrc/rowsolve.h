@@ -70,4 +70,56 @@ __device__ __forceinline__ void row16_sum4(T (&v)[4]) {
   for (int i = 0; i < 4; ++i) v[i] += dpp_step<0x121>(v[i]);
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32-accurate Gram on the bf16 matrix cores.  gfx950's f32-input MFMA runs at the f32
+// vector rate (64 flop/clk/SIMD); v_mfma_f32_16x16x32_bf16 does 16× that.  Each fp32 value
+// is split EXACTLY into three bf16 parts by truncation, x = hi + mid + lo (8 + 8 + 8
+// significand bits), and a product x·y is summed from the six parts of order ≤ 2:
+//   hi·hi + hi·mid + mid·hi + mid·mid + hi·lo + lo·hi
+// (each part product is exact in the fp32 accumulator; the dropped mid·lo + lo·mid + lo·lo
+// are ≤ 2⁻²³ relative — the size of fp32 rounding).  Six 16-cycle MFMAs per 16×16 tile and
+// 32 signals replace eight 32-cycle f32 MFMAs: 2.7× fewer matrix-core cycles.
+// Measured on gfx950 (tools/exp/bf16_layout.hip): Gram error 4.7e-7 of Σ|xᵢxⱼ| vs 2.5e-7
+// for an fp32 FMA chain.
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float trunc_bf16(float x) {
+  return __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+}
+// upper halves of (a, b) packed as two bf16: a in the low half, b in the high half
+__device__ __forceinline__ unsigned pack_hi16(float a, float b) {
+  return (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xffff0000u);
+}
+struct Split3 {
+  u32x4 h, m, l;
+};
+// 8 values (x[0..7]) → three bf16x8 operands with x = h + m + l exactly
+__device__ __forceinline__ void split3(const float (&x)[8], Split3& s) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float x0 = x[2 * p], x1 = x[2 * p + 1];
+    const float r0 = x0 - trunc_bf16(x0), r1 = x1 - trunc_bf16(x1);
+    const float l0 = r0 - trunc_bf16(r0), l1 = r1 - trunc_bf16(r1);
+    s.h[p] = pack_hi16(x0, x1);
+    s.m[p] = pack_hi16(r0, r1);
+    s.l[p] = pack_hi16(l0, l1);
+  }
+}
+__device__ __forceinline__ f32x4 mma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// acc += Xᵢ Xⱼᵀ to fp32 accuracy from the splits of the two row blocks
+__device__ __forceinline__ f32x4 mma_split6(const Split3& a, const Split3& b, f32x4 c) {
+  c = mma_bf16(a.h, b.h, c);
+  c = mma_bf16(a.h, b.m, c);
+  c = mma_bf16(a.m, b.h, c);
+  c = mma_bf16(a.m, b.m, c);
+  c = mma_bf16(a.h, b.l, c);
+  c = mma_bf16(a.l, b.h, c);
+  return c;
+}
+
 }  // namespace qmfx

@@ -35,6 +35,9 @@
 #ifndef QMFX_BIG_SIG64
 #define QMFX_BIG_SIG64 16
 #endif
+#ifndef QMFX_BIG_SPLIT
+#define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
+#endif
 
 namespace qmfx {
 
@@ -44,7 +47,13 @@ struct BigCfg {
   static constexpr int NTT = NT * (NT + 1) / 2;
   // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave
   static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? 4 : 8);
-  static constexpr int TPW = (NTT + NW - 1) / NW;
+  // split-bf16 Gram (fp32, NT = 2·NW): the loader threads split each staged element once
+  // into bf16 hi/mid/lo planes ([column][signal], 32 signals = one 16x16x32 MFMA K step)
+  // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
+  // planes once per stage for both rows
+  static constexpr bool SPLIT = sizeof(T) == 4 && NT == 2 * NW && QMFX_BIG_SPLIT;
+  static constexpr int TPW = SPLIT ? NT + 1 : (NTT + NW - 1) / NW;
+  static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
   static constexpr int SIG = sizeof(T) == 4 ? QMFX_BIG_SIG32 : QMFX_BIG_SIG64;  // signals per LDS stage
   static constexpr int VEC = 16 / sizeof(T);             // elements per 16-B load
@@ -56,14 +65,48 @@ struct BigCfg {
   static constexpr bool REUSE = sizeof(T) == 4 || NT <= 11;
 };
 
+// tile s of wave W: round-robin t = W + NW·s, or (split map) rows W and NT−1−W
+template <typename C>
+__host__ __device__ constexpr void big_tile(int W, int s, int& I, int& J) {
+  if constexpr (C::SPLIT) {
+    constexpr int NT = C::KP / 16;
+    if (s <= W) {
+      I = W;
+      J = s;
+    } else {
+      I = NT - 1 - W;
+      J = s - W - 1;
+    }
+  } else {
+    const int t = W + C::NW * s;
+    if (t < C::NTT) {
+      int i = 0;
+      while ((i + 1) * (i + 2) / 2 <= t) ++i;
+      I = i;
+      J = t - i * (i + 1) / 2;
+    } else {
+      I = J = -1;
+    }
+  }
+}
+
 template <typename T, int NT>
 struct BigShared {
   using C = BigCfg<T, NT>;
-  T stage[2][C::SIG * C::KP];
+  // the Gram staging and the Cholesky panels are never live together
+  union {
+    T stage[2][C::SIG * C::KP];
+    uint16_t planes[2][3][C::SPLIT ? C::KP * C::SPAD : 1];  // split Gram: bf16 hi/mid/lo, [column][signal]
+    float bred[8][C::KP];                    // split Gram: per-wave b partials (after the Gram)
+    struct {
+      T panel[C::KP * C::PLD];
+      T Ldiag[NT * 16 * C::PLD];
+    };
+  };
   T w[2][C::SIG];   // α·v of the staged signals (0 past the row end)
   T c[2][C::SIG];   // 1 + α·v (0 past the row end)
-  T panel[C::KP * C::PLD];
-  T Ldiag[NT * 16 * C::PLD];
+  double cred[8];   // split Gram: per-wave Σc
+  int negw;         // split Gram: some signal has a negative weight (row goes to the re-solve)
   T bw[C::KP];
   T borig[C::KP];
   T xs[C::KP];
@@ -170,13 +213,9 @@ __device__ __forceinline__ void big_gram_step(typename Mfma<T>::acc_t* acc, cons
   }
 #pragma unroll
   for (int s = 0; s < C::TPW; ++s) {
-    const int t = W + C::NW * s;
-    if (t < C::NTT) {
-      int I = 0;
-      while ((I + 1) * (I + 2) / 2 <= t) ++I;
-      const int J = t - I * (I + 1) / 2;
-      acc[s] = M::mma(y[I], wy[J], acc[s]);
-    }
+    int I = -1, J = -1;
+    big_tile<C>(W, s, I, J);
+    if (I >= 0) acc[s] = M::mma(y[I], wy[J], acc[s]);
   }
 }
 
@@ -199,17 +238,58 @@ __device__ __forceinline__ void big_trailing(typename Mfma<T>::acc_t* acc, const
   }
 #pragma unroll
   for (int s = 0; s < C::TPW; ++s) {
-    const int t = W + C::NW * s;
-    if (t < C::NTT) {
-      int I = 0;
-      while ((I + 1) * (I + 2) / 2 <= t) ++I;
-      const int J = t - I * (I + 1) / 2;
-      if (J > p) {
+    int I = -1, J = -1;
+    big_tile<C>(W, s, I, J);
+    if (I >= 0 && J > p) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[s] = M::mma(-fr[I][q], fr[J][q], acc[s]);
-      }
+      for (int q = 0; q < 4; ++q) acc[s] = M::mma(-fr[I][q], fr[J][q], acc[s]);
     }
   }
+}
+
+// Split Gram, MFMA side, for wave W (rows A = W, B = NT−1−W): each column block's planes
+// are read once per stage (three 16-B LDS reads per lane) and used for both rows.
+template <int NT, int W>
+__device__ __forceinline__ void big_split_mfma(f32x4* acc, const uint16_t* pl, int cl, int kk) {
+  using C = BigCfg<float, NT>;
+  constexpr int A = W, B = NT - 1 - W;
+  constexpr int PS = C::KP * C::SPAD;  // one plane
+  auto rd = [&](int X, Split3& sp) {
+    const int off = (16 * X + cl) * C::SPAD + 8 * kk;
+    sp.h = *reinterpret_cast<const u32x4*>(pl + off);
+    sp.m = *reinterpret_cast<const u32x4*>(pl + PS + off);
+    sp.l = *reinterpret_cast<const u32x4*>(pl + 2 * PS + off);
+  };
+  Split3 sa, sb;
+  rd(A, sa);
+  rd(B, sb);
+#pragma unroll
+  for (int J = 0; J <= B; ++J) {
+    Split3 sj;
+    if (J == A) {
+      sj = sa;
+    } else if (J == B) {
+      sj = sb;
+    } else {
+      rd(J, sj);
+    }
+    acc[W + 1 + J] = mma_split6(sb, sj, acc[W + 1 + J]);  // tile (B, J)
+    if (J <= A) acc[J] = mma_split6(sa, sj, acc[J]);      // tile (A, J)
+  }
+}
+
+// 4 fp32 values → their exact bf16 hi/mid/lo parts, packed 2 per word (value 0 in the low
+// half, as split3 packs)
+__device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m, uint2& l) {
+  float r[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = x[j] - trunc_bf16(x[j]);
+    lo[j] = r[j] - trunc_bf16(r[j]);
+  }
+  h = uint2{pack_hi16(x[0], x[1]), pack_hi16(x[2], x[3])};
+  m = uint2{pack_hi16(r[0], r[1]), pack_hi16(r[2], r[3])};
+  l = uint2{pack_hi16(lo[0], lo[1]), pack_hi16(lo[2], lo[3])};
 }
 
 template <typename T, int NT>
@@ -218,7 +298,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   using vec_t = T __attribute__((ext_vector_type(C::VEC)));
-  constexpr int KP = C::KP, NW = C::NW, TPW = C::TPW, NTT = C::NTT, SIG = C::SIG;
+  constexpr int KP = C::KP, NW = C::NW, TPW = C::TPW, SIG = C::SIG;
   constexpr int CPR = C::CPR, TRIPS = C::TRIPS, PLD = C::PLD;
   __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
 
@@ -232,16 +312,10 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   const int64_t beg = a.rowptr[row];
   const int64_t end = a.rowptr[row + 1];
 
-  // this wave's tiles: t = wv + NW·s, (I, J) with t = I(I+1)/2 + J
+  // this wave's tiles (big_tile)
   int TI[TPW], TJ[TPW];
 #pragma unroll
-  for (int s = 0; s < TPW; ++s) {
-    const int t = wv + NW * s;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    TI[s] = t < NTT ? I : -1;
-    TJ[s] = t < NTT ? t - I * (I + 1) / 2 : -1;
-  }
+  for (int s = 0; s < TPW; ++s) big_tile<C>(wv, s, TI[s], TJ[s]);
   acc_t acc[TPW];
 #pragma unroll
   for (int s = 0; s < TPW; ++s) {
@@ -255,6 +329,96 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   }
 
   // ---- Gram: A += Σ w y yᵀ, b = Σ c y, Σc -------------------------------------------------
+  T bp = T(0);        // b[tid] for tid < KP
+  double cs = 0.0;    // Σc (thread 0)
+  int negw = 0;       // split Gram: a negative weight (the split needs √w)
+  if constexpr (C::SPLIT) {
+    // loader thread: column group g (columns 4g..4g+3), signals 4q..4q+3 of each stage
+    const int g = tid & 63, q = tid >> 6;
+    int colq[4];
+    float valq[4];
+    int nval = 0;
+    f32x4 y4[4];
+    float bpart[4] = {0.f, 0.f, 0.f, 0.f};
+    double csl = 0.0;
+    auto load_meta = [&](int64_t sb) {
+      const int64_t e0 = sb + 4 * q;
+      nval = (int)(end - e0 < 0 ? 0 : (end - e0 > 4 ? 4 : end - e0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        colq[j] = j < nval ? a.col[e0 + j] : a.zrow;
+        valq[j] = j < nval ? (float)a.val[e0 + j] : 0.f;
+      }
+    };
+    auto load_rows = [&]() {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        y4[j] = *(reinterpret_cast<const f32x4*>(a.Y + (int64_t)(uint32_t)colq[j] * KP) + g);
+    };
+    auto store_split = [&](int buf) {
+      float sw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float w = (float)a.alpha * valq[j];
+        const float cw = j < nval ? 1.f + w : 0.f;
+        negw |= w < 0.f;
+        sw[j] = fast_sqrt(fabsf(w));
+        if (g == 0) csl += (double)cw;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bpart[m] += cw * y4[j][m];
+      }
+      uint16_t* pl = S.planes[buf][0];
+      constexpr int PS = KP * C::SPAD;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        float x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = sw[j] * y4[j][m];
+        uint2 h, mi, l;
+        split3x4(x, h, mi, l);
+        const int off = (4 * g + m) * C::SPAD + 4 * q;
+        *reinterpret_cast<uint2*>(pl + off) = h;
+        *reinterpret_cast<uint2*>(pl + PS + off) = mi;
+        *reinterpret_cast<uint2*>(pl + 2 * PS + off) = l;
+      }
+    };
+    const int nstages = (int)((end - beg + SIG - 1) / SIG);
+    if (nstages > 0 && !(a.ablate & 1)) {
+      load_meta(beg);
+      load_rows();
+      store_split(0);
+      if (nstages > 1) load_meta(beg + SIG);
+      __syncthreads();
+      for (int st = 0; st < nstages; ++st) {
+        const int buf = st & 1;
+        const bool more = st + 1 < nstages;
+        if (more) load_rows();  // stage st+1 (meta already in registers)
+        auto mf = [&](auto wtag) {
+          big_split_mfma<NT, decltype(wtag)::value>(acc, S.planes[buf][0], cl, kk);
+        };
+        dispatch_wave<NW>(wv, mf);
+        if (more) {
+          store_split(buf ^ 1);
+          if (st + 2 < nstages) load_meta(beg + (int64_t)(st + 2) * SIG);
+        }
+        __syncthreads();
+      }
+    }
+    // b and Σc: per-wave partials in fixed order
+#pragma unroll
+    for (int m = 0; m < 4; ++m) S.bred[q][4 * g + m] = bpart[m];
+    if (lane == 0) S.cred[q] = csl;
+    negw = __syncthreads_or(negw);
+    if (tid < KP) {
+      float b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) b += S.bred[w][tid];
+      bp = b;
+    }
+    if (tid == 0)
+      for (int w = 0; w < 8; ++w) cs += S.cred[w];
+    __syncthreads();
+  } else {
   int cols[TRIPS];
   vec_t stg[TRIPS];
   T wmeta = T(0), cmeta = T(0);
@@ -294,8 +458,6 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     }
   };
 
-  T bp = T(0);        // b[tid] for tid < KP
-  double cs = 0.0;    // Σc (thread 0)
   const int nstages = (int)((end - beg + SIG - 1) / SIG);
   if (nstages > 0 && !(a.ablate & 1)) {
     load_cols(beg);
@@ -347,6 +509,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       __syncthreads();
     }
   }
+  }  // plain Gram
   if (tid < KP) {
     S.bw[tid] = bp;
     S.borig[tid] = bp;
@@ -354,7 +517,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   __syncthreads();
 
   // ---- Cholesky A = L Lᵀ with the forward solve of b folded in --------------------------
-  int bad = 0;
+  int bad = negw ? 1 : 0;  // a negative weight: flagged for the pivoted re-solve
   for (int p = 0; p < NT; ++p) {
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {
@@ -481,11 +644,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void gram_tiles_kernel(
   acc_t acc[TPW];
 #pragma unroll
   for (int s = 0; s < TPW; ++s) {
-    const int t = wv + NW * s;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    TI[s] = t < NTT ? I : -1;
-    TJ[s] = t < NTT ? t - I * (I + 1) / 2 : -1;
+    big_tile<C>(wv, s, TI[s], TJ[s]);
     acc[s] = acc_t{0, 0, 0, 0};
   }
 
