@@ -142,27 +142,46 @@ __device__ void big_panel_head(BigShared<T, NT>& S, int p, int lane, int& bad) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
   T pb = live ? S.bw[16 * p + q] : T(0);
+  // as chol_solve's panel (wals.hip): the column's entries A[m][c] of the diagonal block are
+  // broadcast before the pivot is known (L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]), 1/√d comes
+  // from one reciprocal square root, and 1/L[c][c], y_c stay in lane c until the end
+  T invv = T(0), yv = T(0);
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    const T d = readlane(pa[c], c);
-    bad |= !(d > T(0));
-    const T ljj = fast_sqrt(d);
-    const T inv = fast_rcp(ljj);
-    if (lane == 0) S.invd[16 * p + c] = inv;
-    const T lq = q > c ? pa[c] * inv : T(0);
-    pa[c] = q > c ? lq : (q == c ? ljj : pa[c]);
-    const T yc = readlane(pb, c) * inv;
-    if (lane == 0) S.bw[16 * p + c] = yc;
-    pb -= lq * yc;
+    T am[16];
 #pragma unroll
-    for (int m = c + 1; m < 16; ++m) pa[m] -= lq * readlane(lq, m);
+    for (int m = 1; m < 16; ++m)
+      if (m > c) am[m] = readlane(pa[c], m);
+    const T d = readlane(pa[c], c);
+    const T bc = readlane(pb, c);
+    T ljj, inv;
+    pivot_sqrt(d, ljj, inv);
+    (void)ljj;
+    bad |= !(d > T(0));
+    const bool me = lane == c;
+    invv = me ? inv : invv;
+    yv = me ? bc * inv : yv;
+    // rows below take L[q][c] = A[q][c]/√d (the pivot row √d; rows above: dead upper part)
+    const T lq = pa[c] * inv;
+    const T lqs = lq * inv;
+    pa[c] = lq;
+    pb -= lqs * bc;
+#pragma unroll
+    for (int m = 1; m < 16; ++m)
+      if (m > c) pa[m] -= lqs * am[m];
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if (lane < 16) {
+    S.invd[16 * p + lane] = invv;
+    S.bw[16 * p + lane] = yv;
   }
   if (live) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
     if (q >= 16) S.bw[16 * p + q] = pb;
   }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   for (int idx = lane; idx < 256; idx += 64) {
     const int r = idx >> 4, c = idx & 15;
     S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
@@ -585,15 +604,21 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       T vm = S.bw[16 * I + cl];
 #pragma unroll
       for (int w = 0; w < NW; ++w) vm -= S.part[w * 16 + cl];
+      // row cl scaled by its own 1/L[cl][cl] (x_c is then row c's value itself): each step
+      // is one readlane and one FMA
+      const T dcl = S.invd[16 * I + cl];
       T lc[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) lc[c] = S.Ldiag[(I * 16 + c) * PLD + cl];
+      for (int c = 0; c < 16; ++c) lc[c] = S.Ldiag[(I * 16 + c) * PLD + cl] * dcl;
+      vm *= dcl;
+      T xv = T(0);
 #pragma unroll
       for (int c = 15; c >= 0; --c) {
-        const T xc = readlane(vm, c) * S.invd[16 * I + c];
-        if (lane == 0) S.xs[16 * I + c] = xc;
+        const T xc = readlane(vm, c);
+        xv = lane == c ? xc : xv;
         if (cl < c) vm -= lc[c] * xc;
       }
+      if (lane < 16) S.xs[16 * I + lane] = xv;
     }
     __syncthreads();
   }
