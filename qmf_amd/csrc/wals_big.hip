@@ -353,7 +353,10 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   int negw = 0;       // split Gram: a negative weight (the split needs √w)
   if constexpr (C::SPLIT) {
     // loader thread: column group g (columns 4g..4g+3), signals 4q..4q+3 of each stage
-    const int g = tid & 63, q = tid >> 6;
+    // (KP/4 groups × 8 quads = 32·NT = the workgroup's threads when NT = 2·NW)
+    constexpr int NG4 = KP / 4;
+    static_assert(NG4 * 8 == C::NTHR, "split loader: one (column group, quad) per thread");
+    const int g = tid % NG4, q = tid / NG4;
     int colq[4];
     float valq[4];
     int nval = 0;
@@ -426,7 +429,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     // b and Σc: per-wave partials in fixed order
 #pragma unroll
     for (int m = 0; m < 4; ++m) S.bred[q][4 * g + m] = bpart[m];
-    if (lane == 0) S.cred[q] = csl;
+    if (g == 0) S.cred[q] = csl;
     negw = __syncthreads_or(negw);
     if (tid < KP) {
       float b = 0.f;

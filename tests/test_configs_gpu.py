@@ -53,6 +53,7 @@ def test_config_shape_lockstep_halves(c_shape, cfg, k, precision):
         side = h % 2
         lo = o.iterate(side, NTHR)
         ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+        assert len(c.failed_rows()) == 0, (cfg, h)  # SPD rows: no pivoted re-solve
         err = rel_err(c.factors(side), o.factors(side))
         assert err < tol, (cfg, h, err)
         assert abs(ld - lo) < tol * abs(lo), (cfg, h, ld, lo)
