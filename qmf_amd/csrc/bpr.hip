@@ -58,6 +58,20 @@ __device__ __forceinline__ void add_row(const Row<T, E>& r, const Row<T, E>& r0,
     if (lane + 64 * e < kp) unsafeAtomicAdd(base + lane + 64 * e, r.v[e] - r0.v[e]);
 }
 
+// x̂ of one (u, p, n) step summed over the wave: 16-lane DPP row sums, then the four rows'
+// sums in a fixed order (no LDS round trips; the value is wave-uniform)
+template <typename T>
+__device__ __forceinline__ T wave_total(T v) {
+  v = row16_sum(v);
+  return (readlane(v, 0) + readlane(v, 16)) + (readlane(v, 32) + readlane(v, 48));
+}
+// lossDerivative (BPREngine.cpp:240-244): 1 / (1 + e^x̂).  fp32: the hardware exp2 and
+// reciprocal (≤ 1 ulp each); fp64: exact library calls
+__device__ __forceinline__ float neg_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(x));
+}
+__device__ __forceinline__ double neg_sigmoid(double x) { return 1.0 / (1.0 + exp(x)); }
+
 // One SGD step on (u, p, n).  Returns false if the derivative was not finite.
 template <typename T, int E>
 __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t p, int64_t n,
@@ -70,15 +84,14 @@ __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t
   T part = T(0);
 #pragma unroll
   for (int e = 0; e < E; ++e) part += pu.v[e] * (qp.v[e] - qn.v[e]);
-  T x = wave_sum(part);
+  T x = wave_total(part);
   T bp = T(0), bn = T(0);
   if (a.use_biases) {
     bp = ld_shared(a.bias + p);
     bn = ld_shared(a.bias + n);
     x += bp - bn;
   }
-  const T ex = exp(x);
-  const T eg = T(1) / (T(1) + ex);
+  const T eg = neg_sigmoid(x);
   if (!isfinite(eg)) return false;
   const T lr = a.lr;
   // p == n (possible only in a caller-given sequence: sampled negatives are never positives):
@@ -106,14 +119,34 @@ __device__ __forceinline__ bool bpr_step(const BprArgs<T>& a, int64_t u, int64_t
   return true;
 }
 
+// murmur3 32-bit finaliser (a bijection of uint32)
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  return x ^ (x >> 16);
+}
+
+// Negative sampling (sampleRandomNegative, BPREngine-inl.h:48-60, which draws from
+// mt19937): counter-based instead, so every draw is reproducible for a given seed.  Positive
+// slot s has the 64-bit key mix64(seed_key ^ s) (one splitmix64 per positive); draw j,
+// attempt t of it is fmix32(fold(key) + (4099·j + t)·φ) scaled to [0, nitems) — a bijection
+// of the counter, all in 32-bit scalar arithmetic.
+__device__ __forceinline__ uint32_t draw_hash(uint32_t fk, uint32_t ctr) {
+  return fmix32(fk + ctr * 0x9e3779b9u);
+}
+__device__ __forceinline__ int64_t draw_candidate(uint32_t fk, uint32_t ctr, uint32_t nitems) {
+  return (int64_t)(((uint64_t)draw_hash(fk, ctr) * nitems) >> 32);
+}
+
 // Rejection-samples a negative for user u: uniform in [0, nitems) and not in the user's
-// positive set (sorted list urowptr/uitems).  Counter-based, so every (positive, j) draw is
-// reproducible for a given seed.
+// positive set (sorted list urowptr/uitems).  fk = the positive's folded key, ctr0 = 4099·j.
 __device__ __forceinline__ int64_t sample_negative(const int32_t* items, int64_t cnt,
-                                                   int64_t nitems, uint64_t key, int lane) {
+                                                   uint32_t nitems, uint32_t fk, uint32_t ctr0,
+                                                   int lane) {
   for (uint32_t attempt = 0;; ++attempt) {
-    const uint64_t h = mix64(key ^ ((uint64_t)attempt << 48) ^ 0x5bd1e995ull);
-    const int64_t cand = (int64_t)(((unsigned __int128)h * (uint64_t)nitems) >> 64);
+    const int64_t cand = draw_candidate(fk, ctr0 + attempt, nitems);
     bool hit = false;
     for (int64_t base = 0; base < cnt; base += 64) {
       const int64_t j = base + lane;
@@ -131,11 +164,12 @@ __device__ __forceinline__ int64_t sample_negative(const int32_t* items, int64_t
 // `mine` (one per lane); longer lists are scanned from memory.
 template <typename A>
 __device__ __forceinline__ int64_t draw_negative_t(const A& a, const int32_t* items, int64_t cnt,
-                                                   int32_t mine, uint64_t key, int lane) {
-  if (cnt > 64) return sample_negative(items, cnt, a.nitems, key, lane);
+                                                   int32_t mine, uint32_t fk, uint32_t ctr0,
+                                                   int lane) {
+  const uint32_t ni = (uint32_t)a.nitems;
+  if (cnt > 64) return sample_negative(items, cnt, ni, fk, ctr0, lane);
   for (uint32_t attempt = 0;; ++attempt) {
-    const uint64_t h = mix64(key ^ ((uint64_t)attempt << 48) ^ 0x5bd1e995ull);
-    const int64_t cand = (int64_t)(((unsigned __int128)h * (uint64_t)a.nitems) >> 64);
+    const int64_t cand = draw_candidate(fk, ctr0 + attempt, ni);
     if (!__any(mine == (int32_t)cand) || attempt >= 4096) return cand;
   }
 }
@@ -184,9 +218,9 @@ __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int
     T part = T(0);
 #pragma unroll
     for (int e = 0; e < E; ++e) part += pu.v[e] * (qp.v[e] - qn[j].v[e]);
-    T x = wave_sum(part);
+    T x = wave_total(part);
     if (a.use_biases) x += bp - bn[j];
-    const T eg = T(1) / (T(1) + exp(x));
+    const T eg = neg_sigmoid(x);
     if (!isfinite(eg)) {
       ok = false;
       continue;  // the reference aborts (CHECK); the row is left as it was
@@ -243,6 +277,7 @@ __global__ __launch_bounds__(64) void bpr_epoch_kernel(BprArgs<T> a) {
   int64_t i = blockIdx.x;
   if (i >= a.npos) return;
   bool ok = true;
+  const uint64_t seed_key = mix64(a.seed ^ 0xb5ad4eceda1ce2a9ull);
   // stage 0 (current): everything; stage 1: + CSR range; stage 2: (user, item)
   uint64_t s0 = (uint64_t)(((unsigned __int128)a.perm_a * (uint64_t)i + a.perm_b) % np);
   uint64_t s1 = advance(s0), s2 = advance(s1), s3 = s2;
@@ -260,15 +295,15 @@ __global__ __launch_bounds__(64) void bpr_epoch_kernel(BprArgs<T> a) {
     const int64_t u3 = a.pos_user[slot3], p3 = a.pos_item[slot3];
     const int64_t rb2 = a.urowptr[u2], cnt2 = a.urowptr[u2 + 1] - rb2;
     int32_t mine1 = a.uitems[rb1 + (lane < cnt1 ? lane : 0)];
+    const uint64_t pkey = mix64(seed_key ^ (uint64_t)slot0);
+    const uint32_t fk = (uint32_t)pkey ^ (uint32_t)(pkey >> 32);
     for (int j0 = 0; j0 < a.num_neg; j0 += 4) {
       const int nn = a.num_neg - j0 < 4 ? a.num_neg - j0 : 4;
       int64_t n[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (j < nn) {
-          const uint64_t key = mix64(a.seed ^ mix64((uint64_t)slot0 * 64ull + (uint64_t)(j0 + j)));
-          n[j] = draw_negative_t(a, a.uitems + rb0, cnt0, mine0, key, lane);
-        }
+        if (j < nn)
+          n[j] = draw_negative_t(a, a.uitems + rb0, cnt0, mine0, fk, 4099u * (uint32_t)(j0 + j), lane);
       ok &= bpr_positive<T, E>(a, u0, p0, n, nn, lane);
     }
     mine1 = lane < cnt1 ? mine1 : -1;

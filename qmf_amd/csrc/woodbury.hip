@@ -290,6 +290,260 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Whitened row kernel, streamed (fp32, k ≤ 128): the n×n solve of wals_woodbury_kernel
+// without holding Zₛ in registers.  K = Zₛ Zₛᵀ accumulates over 32-column chunks of the
+// gathered rows — each chunk split into bf16 parts as it arrives, the next chunk in flight —
+// and x' = Zₛᵀu gathers the rows a second time after the solve, from the L2 / MALL (the same
+// rows were read a few µs earlier).  Lane (i, g) holds columns 32s + 8g .. +7 of signal
+// 16I + i in chunk s.  ≈150 VGPRs instead of 256 at NTN = 4: three waves per SIMD.
+// ---------------------------------------------------------------------------------------
+#ifndef QMFX_WB_ST_WAVES
+#define QMFX_WB_ST_WAVES 3
+#endif
+template <int NTK, int NTN>
+__global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(SolveArgs<float> a) {
+  using M = Mfma<float>;
+  using acc_t = f32x4;
+  constexpr int KP = 16 * NTK;
+  constexpr int NTT = NTN * (NTN + 1) / 2;
+  constexpr int NS = (KP + 31) / 32;
+  __shared__ __attribute__((aligned(16))) CholShared<float, NTN> S;
+  __shared__ __attribute__((aligned(16))) float gq[16 * NTN];
+
+  const int lane = threadIdx.x;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
+  const int64_t row = dn.row;
+  const int n = dn.n;  // ≤ 16·NTN by bucketing
+  const bool mine = lane < n;
+  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
+  const float vr = mine ? a.val[dn.beg + lane] : 0.f;
+  const float wl = mine ? a.alpha * vr : 0.f;
+  const float cwl = mine ? 1.f + a.alpha * vr : 0.f;
+  const bool isP = mine && wl > 0.f;
+  const bool isQ = mine && wl == 0.f;
+  int bad = __any(mine && wl < 0.f) ? 1 : 0;
+  const uint64_t mQ = __ballot(isQ);
+  const bool hasQ = mQ != 0;
+
+  // this lane's signals 16I + cl (padding signals read the all-zero row a.zrow)
+  const f32x4* zp[NTN];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int ce = __shfl(cr, 16 * I + cl, 64);
+    zp[I] = reinterpret_cast<const f32x4*>(a.Y + (uint64_t)(uint32_t)ce * KP);
+  }
+  auto load_chunk = [&](int s, f32x4 (&buf)[NTN][2]) {
+    const int c4 = 8 * s + 2 * kk;  // f32x4 index of column 32s + 8kk
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      if (32 * s + 32 <= KP || 32 * s + 8 * kk < KP) {
+        buf[I][0] = zp[I][c4];
+        buf[I][1] = zp[I][c4 + 1];
+      } else {
+        buf[I][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        buf[I][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  acc_t acc[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0.f, 0.f, 0.f, 0.f};
+  float sq[NTN];  // z_eᵀ Σ_{f∈Q} z_f over this lane's columns (rows with Q signals)
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) sq[I] = 0.f;
+  {
+    f32x4 cur[NTN][2], nxt[NTN][2];
+    load_chunk(0, cur);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      Split3 sp[NTN];
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+        float x[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          x[c] = cur[I][0][c];
+          x[4 + c] = cur[I][1][c];
+        }
+        split3(x, sp[I]);
+      }
+      if (hasQ) {
+        float g[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float v = 0.f;
+#pragma unroll
+            for (int I = 0; I < NTN; ++I)
+              if ((mQ >> (16 * I + cl)) & 1) v += cur[I][h][c];
+            g[h][c] = v;
+          }
+        row16_sum4(g[0]);
+        row16_sum4(g[1]);
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sq[I] += cur[I][h][c] * g[h][c];
+      }
+#pragma unroll
+      for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+          acc[t] = mma_split6(sp[I], sp[J], acc[t]);
+        }
+      }
+      if (s + 1 < NS) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) {
+          cur[I][0] = nxt[I][0];
+          cur[I][1] = nxt[I][1];
+        }
+      }
+      // one chunk's splits and the next chunk's loads live at a time
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  double xb = 0.0;
+  float ul[NTN], cv[NTN];
+  if (!hasQ) {
+    const float iw = isP ? fast_rcp(wl) : 1.f;
+    const float rhs = isP ? cwl * iw : 0.f;
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const float iwd = __shfl(iw, 16 * I + cl, 64);
+      const int t = tile_index(I, I);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : 0.f;
+    }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    __syncthreads();
+    chol_solve<float, NTN>(acc, S, lane, bad);
+    const float ue = lane < 16 * NTN ? S.xs[lane] : 0.f;
+    xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      ul[I] = S.xs[16 * I + cl];
+      cv[I] = 0.f;
+    }
+  } else {
+    float rhs = isP ? cwl * fast_rcp(wl) : 0.f;
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      float v = sq[I];
+      v += shfl_xor(v, 16);
+      v += shfl_xor(v, 32);
+      if (kk == 0) gq[16 * I + cl] = v;
+    }
+    __syncthreads();
+    const float kqv = lane < 16 * NTN ? gq[lane] : 0.f;
+    if (isP) rhs -= kqv;
+    const float iw = isP ? fast_rcp(wl) : 0.f;
+    const uint64_t mP = __ballot(isP);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const float iwd = __shfl(iw, 16 * I + cl, 64);
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        const int f = 16 * J + cl;
+        const bool pf = (mP >> f) & 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = 16 * I + M::crow(lane, r);
+          const bool pe = (mP >> e) & 1;
+          float v = acc[t][r];
+          if (pe && pf) v += (e == f) ? iwd : 0.f;
+          else v = (e == f) ? 1.f : 0.f;
+          acc[t][r] = v;
+        }
+      }
+    }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    __syncthreads();
+    chol_solve<float, NTN>(acc, S, lane, bad);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const int e = 16 * I + cl;
+      const bool pe = (mP >> e) & 1;
+      const bool qe = (mQ >> e) & 1;
+      ul[I] = pe ? S.xs[e] : (qe ? 1.f : 0.f);
+      cv[I] = __shfl(cwl, e, 64);
+    }
+  }
+
+  // x' = Zₛᵀu (and for rows with Q signals xᵀb = x'ᵀ(Zₛᵀc)), the rows gathered again
+  {
+    f32x4 cur[NTN][2], nxt[NTN][2];
+    load_chunk(0, cur);
+    double xbq = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      float sx[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v = 0.f;
+#pragma unroll
+          for (int I = 0; I < NTN; ++I) v += cur[I][h][c] * ul[I];
+          sx[h][c] = v;
+        }
+      row16_sum4(sx[0]);
+      row16_sum4(sx[1]);
+      if (hasQ) {
+        float sb[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float v = 0.f;
+#pragma unroll
+            for (int I = 0; I < NTN; ++I) v += cur[I][h][c] * cv[I];
+            sb[h][c] = v;
+          }
+        row16_sum4(sb[0]);
+        row16_sum4(sb[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) xbq += (double)sx[h][c] * (double)sb[h][c];
+      }
+      // lanes cl = 0, 1 of each 16-lane row store columns 32s + 8kk + 4cl .. +3
+      if (cl < 2 && 32 * s + 8 * kk < KP) {
+        f32x4 o = cl == 0 ? f32x4{sx[0][0], sx[0][1], sx[0][2], sx[0][3]}
+                          : f32x4{sx[1][0], sx[1][1], sx[1][2], sx[1][3]};
+        if (bad) o = f32x4{0.f, 0.f, 0.f, 0.f};
+        reinterpret_cast<f32x4*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
+      }
+      if (s + 1 < NS) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) {
+          cur[I][0] = nxt[I][0];
+          cur[I][1] = nxt[I][1];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
+  }
+  const double csum = wave_sum((double)cwl);
+  if (lane == 0) {
+    a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
+    if (bad && a.status) a.status[row] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Whitened row kernel, multi-wave: the same n×n solve as wals_woodbury_kernel for factor
 // counts whose whitened rows do not fit one wave's registers (fp64 k > 64, fp32 k = 256).
 // One workgroup of NWK waves per row; wave w holds the column blocks q = w·KW .. w·KW+KW-1
@@ -683,11 +937,39 @@ __global__ __launch_bounds__(256) void chol_inv_kernel(const T* G, int k, double
 
 
 #ifndef QMFX_KERNELS_ONLY
+// fp32 k ≤ 128: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
+static bool wb_stream() {
+  const char* e = std::getenv("QMFX_WB_STREAM");
+  return !e || std::atoi(e) != 0;
+}
+
 template <typename T, int NTK>
 static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
+  if constexpr (sizeof(T) == 4 && NTK <= 8) {
+    if (!a.trace && wb_stream()) {
+#define QMFX_WBS(N)                                                                        \
+  return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                             \
+    hipLaunchKernelGGL((wals_woodbury_st_kernel<NTK, N>), dim3((unsigned)c.nrows), b, 0, s, c); \
+  })
+      switch (ntn) {
+        case 1: QMFX_WBS(1);
+        case 2:
+          if constexpr (NTK >= 4) QMFX_WBS(2);
+          return hipErrorInvalidValue;
+        case 3:
+          if constexpr (NTK >= 6) QMFX_WBS(3);
+          return hipErrorInvalidValue;
+        case 4:
+          if constexpr (NTK >= 8) QMFX_WBS(4);
+          return hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+      }
+#undef QMFX_WBS
+    }
+  }
 #define QMFX_WB(N)                                                                            \
   return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                                \
     if (c.trace)                                                                              \

@@ -3,8 +3,9 @@
 With min(nusers, nitems) < 32 the epoch runs on one wave, i.e. serially, as the reference's
 1-thread Hogwild (BPREngine::optimize/iterateBlock, BPREngine.cpp:146-176, -inl.h:31-46).
 The visiting order (identity, or the seeded affine permutation when shuffling) and every
-negative (counter-based draw, rejected against the user's positives; -inl.h:48-60 draws
-from mt19937 instead, so the stream itself is this build's) are restated here; the
+negative (counter-based draw: one splitmix64 key per positive, a murmur3 finaliser per
+attempt, rejected against the user's positives; -inl.h:48-60 draws from mt19937 instead, so
+the stream itself is this build's) are restated here; the
 resulting (u, p, n) sequence run through the oracle's BPREngine::update
 (BPREngine.cpp:178-220) must reproduce the device's factors and biases.  Tolerance: fp64
 1e-12, fp32 1e-5 relative."""
@@ -16,6 +17,7 @@ import qmf_amd
 
 pytestmark = pytest.mark.gpu
 M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
 
 
 def mix64(x):
@@ -23,6 +25,14 @@ def mix64(x):
     x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
     x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
     return x ^ (x >> 31)
+
+
+def fmix32(x):
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & M32
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & M32
+    return x ^ (x >> 16)
 
 
 def permutation(seed, npos, shuffle):
@@ -42,16 +52,18 @@ def triplets(users, items, nitems, seed, num_neg, shuffle):
     for u, i in zip(users, items):
         pos.setdefault(int(u), set()).add(int(i))
     pa, pb = permutation(seed, npos, shuffle)
+    seed_key = mix64(seed ^ 0xB5AD4ECEDA1CE2A9)
     out = []
     for i in range(npos):
         slot = (pa * i + pb) % npos
         u, p = int(users[slot]), int(items[slot])
+        pkey = mix64(seed_key ^ slot)
+        fk = (pkey & M32) ^ (pkey >> 32)
         for j in range(num_neg):
-            key = mix64((seed ^ mix64((slot * 64 + j) & M64)) & M64)
             attempt = 0
             while True:
-                h = mix64(key ^ ((attempt << 48) & M64) ^ 0x5BD1E995)
-                cand = (h * nitems) >> 64
+                h = fmix32((fk + ((4099 * j + attempt) * 0x9E3779B9)) & M32)
+                cand = (h * nitems) >> 32
                 if cand not in pos[u] or attempt >= 4096:
                     break
                 attempt += 1
