@@ -85,17 +85,22 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   float cs = 0.f;
   int pc = a.zrow;
   float pv = 0.f;
-  auto fetch = [&](int ch) {  // this lane's signal of chunk ch → (pc, pv)
+  // Every load below is issued unconditionally (past the row's end from a clamped address;
+  // stage() then substitutes the zero row): a load skipped on some path makes the compiler's
+  // waitcnt merge assume the shortest queue, and then each step waited for the gathers of
+  // the step after it (the whole gather latency exposed twice per 64 signals).
+  auto fetch = [&](int ch) {  // this lane's signal of chunk ch → raw (pc, pv)
     const int e = 64 * ch + lane;
-    const bool ok = e < n;
-    pc = ok ? a.col[beg + e] : a.zrow;
-    pv = ok ? a.val[beg + e] : 0.f;
+    const int64_t src = beg + (e < n ? e : 0);
+    pc = a.col[src];
+    pv = a.val[src];
   };
   auto stage = [&](int ch) {  // (pc, pv) of chunk ch → LDS
     const bool ok = 64 * ch + lane < n;
-    cs += ok ? 1.f + a.alpha * pv : 0.f;
-    mcol[ch & 1][lane] = pc;
-    mval[ch & 1][lane] = pv;
+    const float v = ok ? pv : 0.f;
+    cs += ok ? 1.f + a.alpha * v : 0.f;
+    mcol[ch & 1][lane] = ok ? pc : a.zrow;
+    mval[ch & 1][lane] = v;
   };
   auto read_meta = [&](int st, int (&col)[8], float (&val)[8]) {
     const int o = 32 * (st & 1) + 8 * g;
@@ -123,31 +128,37 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
     }
   };
   if (nsteps == 0) return;
-  // prologue: chunks 0 (and 1) staged, chunk 2 in flight, step 0's rows in flight
+  // prologue: chunks 0 and 1 staged (a chunk past the end as zero-row signals), chunk 2 in
+  // flight, step 0's rows in flight
   fetch(0);
   stage(0);
-  if (nchunks > 1) {
-    fetch(1);
-    stage(1);
-  }
-  if (nchunks > 2) fetch(2);
+  fetch(1);
+  stage(1);
+  fetch(2);
   // One step: the next step's rows go out first (into the other buffer, whose rows were
   // consumed one step ago), then each block is split right before the tiles of its block
   // row, so the split VALU of block I+1 issues in the free cycles of row I's MFMAs.  The
   // two buffers swap roles by a 2× unroll (no register copies).
   auto step = [&](int st, vecW (&yc)[8][NG], float (&vc)[8], vecW (&yn)[8][NG],
                   float (&vn)[8]) {
-    if (st + 1 < nsteps) {
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      // (unconditional: past the last step this stages / fetches / gathers zero-row or
+      // already-consumed signals whose results are never used)
       if (((st + 1) & 1) == 0) {
         // step st+1 opens chunk k = (st+1)/2: stage chunk k+1, fetch chunk k+2
         const int k = (st + 1) >> 1;
-        if (k + 1 < nchunks) stage(k + 1);
-        if (k + 2 < nchunks) fetch(k + 2);
+        stage(k + 1);
+        fetch(k + 2);
       }
       int cn[8];
       read_meta(st + 1, cn, vn);
       load_rows(cn, yn);
     }
+    // the next step's gathers all leave before this step's MFMAs start: each then has a
+    // whole step to land (scheduled freely they trickled out between the MFMAs, the last
+    // ones right before the next step waits on them)
+    __builtin_amdgcn_sched_barrier(0);
     float sw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -187,9 +198,11 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   vecW y0[8][NG], y1[8][NG];
   read_meta(0, col0, val0);
   load_rows(col0, y0);
-  for (int st = 0; st < nsteps; st += 2) {
+  // an even number of steps (a row with an odd count runs one step of zero-row signals), so
+  // the loop body has no branch between the loads and their consumers
+  for (int st = 0; st < 2 * nchunks; st += 2) {
     step(st, y0, val0, y1, val1);
-    if (st + 1 < nsteps) step(st + 1, y1, val1, y0, val0);
+    step(st + 1, y1, val1, y0, val0);
   }
   const double tot = wave_sum((double)cs);
   csum += lane == 0 ? tot : 0.0;  // the caller sums the cl == 0 lanes
