@@ -22,6 +22,7 @@
 // interactions CSR (int64 rowptr, int32 column, value v).  The padded part of every system
 // is the identity, so padded solution entries are exactly zero.
 #include <algorithm>
+#include <utility>
 #include <cstdlib>
 
 #include "common.h"
@@ -208,6 +209,161 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   csum += lane == 0 ? tot : 0.0;  // the caller sums the cl == 0 lanes
 }
 
+// Direct-row Gram without the split (fp64, and fp32 at k ≤ 80): one 16x16x4 MFMA per tile
+// per 4 signals, straight from the gathered rows.  Signals come in chunks of 64: lane (l, g)
+// holds the (column, value) of signal 64c + g·S + l, where S = the chunk's step count (16;
+// in a final partial chunk ⌈rest/4⌉ rounded up to PD), so step j's signal of lane group g
+// sits in lane j of the same 16-lane row.  In the full chunks it arrives by one DPP row
+// broadcast (compile-time lane, the chunk's 16 steps in straight line); the partial last
+// chunk runs a loop of PD-step groups with shuffles.  The rows of step j + PD are gathered
+// while step j's MFMAs run (PD register buffers); every load is issued unconditionally (past
+// the end from a clamped address, replaced by the all-zero row a.zrow at use) and each step
+// is its own scheduling region, so a step waits only for the buffer it consumes.  The next
+// chunk's (column, value) pairs are loaded a whole chunk ahead.
+template <typename T, int NT>
+constexpr int plain_depth() {
+  return (sizeof(T) == 8 && NT > 4) ? 2 : 4;  // fp64 k > 64: one wave with the whole file
+}
+template <int J>
+__device__ __forceinline__ int row_bcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, false);
+}
+template <int J>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __int_as_float(row_bcast<J>(__float_as_int(v)));
+}
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = row_bcast<J>((int)(b & 0xffffffffll));
+  const int hi = row_bcast<J>((int)(b >> 32));
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
+template <typename T, int NT, int PD>
+__device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, int n,
+                                           typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
+                                           T (&bpart)[NT], double& csum, int lane) {
+  using M = Mfma<T>;
+  constexpr int KP = 16 * NT;
+  static_assert(16 % PD == 0, "the ring must tile a chunk");
+  const int cl = lane & 15;
+  const int g = lane >> 4;
+  if (n <= 0) return;
+  const int nfull = n >> 6;
+  // steps of chunk c: 16, or the partial chunk's ⌈rest/4⌉ rounded up to a multiple of PD
+  // (0 past the end)
+  auto steps_of = [&](int c) {
+    const int rest = n - 64 * c;
+    if (rest >= 64) return 16;
+    const int st = rest > 0 ? (rest + 3) >> 2 : 0;
+    return ((st + PD - 1) / PD) * PD;
+  };
+  // raw (clamped) loads of this lane's signal of chunk c; validity is re-derived at use
+  auto load_chunk = [&](int c, int& cr, T& vr) {
+    const int S = steps_of(c);
+    const int e = 64 * c + g * S + cl;
+    const int64_t src = beg + ((cl < S && e < n) ? e : 0);
+    cr = a.col[src];
+    vr = a.val[src];
+  };
+  T yb[PD][NT];
+  T wb[PD], cwb[PD];
+  // gather step j (its column cj / value vj broadcast from lane j of the row) into buffer b
+  auto gather = [&](bool ok, int cj, T vj, int b) {
+    const int col = ok ? cj : a.zrow;
+    const T v = ok ? vj : T(0);
+    wb[b] = a.alpha * v;
+    cwb[b] = ok ? T(1) + a.alpha * v : T(0);
+    const T* yrow = a.Y + (uint64_t)(uint32_t)col * KP + cl;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) yb[b][q] = yrow[16 * q];
+  };
+  // step J of a chunk whose lane (l, g) signals start at base = 64c + g·S (S steps)
+  auto issue = [&](auto Jc, int S, int base, int cr, T vr, int b) {
+    constexpr int J = decltype(Jc)::value;
+    // pinned here: hoisted to the chunk's start, 16 steps of broadcasts and addresses
+    // stayed live across it (and spilled)
+    int crx = cr;
+    T vrx = vr;
+    asm volatile("" : "+v"(crx), "+v"(vrx));
+    gather(J < S && base + J < n, row_bcast<J>(crx), row_bcast<J>(vrx), b);
+  };
+  auto consume = [&](int b) {
+    const T w = wb[b], cw = cwb[b];
+    T wy[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      bpart[q] += cw * yb[b][q];
+      wy[q] = w * yb[b][q];
+    }
+    csum += (double)cw;
+    // pinned to the step: otherwise the rhs FMAs sink to the chunk's end and every step's
+    // rows stay live (spilled) until then
+#pragma unroll
+    for (int q = 0; q < NT; ++q) asm volatile("" : "+v"(bpart[q]));
+    asm volatile("" : "+v"(csum));
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J2 = 0; J2 <= I; ++J2) {
+        const int t = tile_index(I, J2);
+        acc[t] = M::mma(yb[b][I], wy[J2], acc[t]);
+      }
+    }
+  };
+  int cr, crn;
+  T vr, vrn;
+  load_chunk(0, cr, vr);
+  load_chunk(1, crn, vrn);
+  {
+    const int S0 = steps_of(0);
+    const int base0 = g * S0;
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (issue(std::integral_constant<int, P>{}, S0, base0, cr, vr, P), ...);
+    }(std::make_integer_sequence<int, PD>{});
+  }
+  // full chunks: 16 steps in straight line
+  for (int c = 0; c < nfull; ++c) {
+    const int base = 64 * c + 16 * g;
+    const int Sn = steps_of(c + 1);
+    const int basen = 64 * (c + 1) + g * Sn;
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      auto one = [&](auto Jc) {
+        constexpr int j = decltype(Jc)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        consume(j % PD);
+        if constexpr (j + PD < 16)
+          issue(std::integral_constant<int, j + PD>{}, 16, base, cr, vr, j % PD);
+        else
+          issue(std::integral_constant<int, j + PD - 16>{}, Sn, basen, crn, vrn, j % PD);
+      };
+      (one(std::integral_constant<int, J>{}), ...);
+    }(std::make_integer_sequence<int, 16>{});
+    __builtin_amdgcn_sched_barrier(0);
+    cr = crn;
+    vr = vrn;
+    load_chunk(c + 2, crn, vrn);
+  }
+  // the partial chunk (its first PD steps already in the buffers)
+  const int St = steps_of(nfull);
+  const int baset = 64 * nfull + g * St;
+  for (int j0 = 0; j0 < St; j0 += PD) {
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      auto one = [&](auto Pc) {
+        constexpr int b = decltype(Pc)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        consume(b);
+        const int j = j0 + b + PD;  // next step for this buffer (lane j of the row)
+        const int src = (g << 4) + (j & 15);
+        gather(j < St && baset + j < n, __shfl(cr, src, 64), __shfl(vr, src, 64), b);
+      };
+      (one(std::integral_constant<int, P>{}), ...);
+    }(std::make_integer_sequence<int, PD>{});
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // ---------------------------------------------------------------------------------------
 // Direct row kernel: one wave64 per row (slot order heaviest-first).  Gram
 // A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in registers, starting from
@@ -223,7 +379,7 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 // keep their accumulators in the whole (VGPR + AGPR) register file of one wave
 template <typename T, int NT>
 constexpr int direct_waves() {
-  return Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : (sizeof(T) == 8 && NT > 4 ? 1 : 2);
+  return Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : (sizeof(T) == 8 && NT > 4 ? 1 : (NT <= 4 ? 4 : 2));
 }
 
 template <typename T, int NT, bool TRACE>
@@ -288,47 +444,52 @@ void wals_direct_kernel(SolveArgs<T> a) {
     int negw = 0;
     if constexpr (Perm<NT>::template split<T>) {
       gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
-    } else
-    for (int64_t base = beg; base < end; base += 64) {
-      const int nst = (int)(end - base < 64 ? end - base : 64);
-      const int cr = lane < nst ? a.col[base + lane] : 0;
-      const T vr = lane < nst ? a.val[base + lane] : T(0);
-      bool valid = kk < nst;
-      T v = __shfl(vr, kk, 64);
-      T yn[NT];
-      {
-        const T* yrow = a.Y + (uint64_t)(uint32_t)__shfl(cr, kk, 64) * KP + cl;
-#pragma unroll
-        for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
-      }
-      for (int s = 0; 4 * s < nst; ++s) {
-        T yv[NT];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
-        const T w = valid ? a.alpha * v : T(0);
-        const T cw = valid ? T(1) + a.alpha * v : T(0);
-        const int jn = 4 * (s + 1) + kk;
-        const bool vn = jn < nst;
-        if (4 * (s + 1) < nst) {
-          const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
-          v = __shfl(vr, jn < 64 ? jn : 0, 64);
-          const T* yrow = a.Y + (uint64_t)(uint32_t)(vn ? cn : cr) * KP + cl;
+    } else if constexpr (sizeof(T) == 8 && NT > 4) {
+      // fp64 k > 64 (one wave, accumulators across the whole register file): the ring of
+      // gram_plain costs more spills than its deeper prefetch gains; one step ahead
+      for (int64_t base = beg; base < end; base += 64) {
+        const int nst = (int)(end - base < 64 ? end - base : 64);
+        const int cr = lane < nst ? a.col[base + lane] : 0;
+        const T vr = lane < nst ? a.val[base + lane] : T(0);
+        bool valid = kk < nst;
+        T v = __shfl(vr, kk, 64);
+        T yn[NT];
+        {
+          const T* yrow = a.Y + (uint64_t)(uint32_t)__shfl(cr, kk, 64) * KP + cl;
 #pragma unroll
           for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
         }
-        valid = vn;
+        for (int s = 0; 4 * s < nst; ++s) {
+          T yv[NT];
 #pragma unroll
-        for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
-        csum += (double)cw;
+          for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
+          const T w = valid ? a.alpha * v : T(0);
+          const T cw = valid ? T(1) + a.alpha * v : T(0);
+          const int jn = 4 * (s + 1) + kk;
+          const bool vn = jn < nst;
+          if (4 * (s + 1) < nst) {
+            const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
+            v = __shfl(vr, jn < 64 ? jn : 0, 64);
+            const T* yrow = a.Y + (uint64_t)(uint32_t)(vn ? cn : cr) * KP + cl;
 #pragma unroll
-        for (int I = 0; I < NT; ++I) {
+            for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
+          }
+          valid = vn;
 #pragma unroll
-          for (int J = 0; J <= I; ++J) {
-            const int t = tile_index(I, J);
-            acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+          for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
+          csum += (double)cw;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+              const int t = tile_index(I, J);
+              acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+            }
           }
         }
       }
+    } else {
+      gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
     }
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
