@@ -300,6 +300,10 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 #ifndef QMFX_WB_ST_WAVES
 #define QMFX_WB_ST_WAVES 3
 #endif
+// K on the bf16 matrix cores from split3 parts (1) or on the f32 matrix path (0)
+#ifndef QMFX_WBS_SPLIT
+#define QMFX_WBS_SPLIT 1
+#endif
 template <int NTK, int NTN>
 __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(SolveArgs<float> a) {
   using M = Mfma<float>;
@@ -360,6 +364,7 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (s + 1 < NS) load_chunk(s + 1, nxt);
+#if QMFX_WBS_SPLIT
       Split3 sp[NTN];
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
@@ -371,6 +376,7 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
         }
         split3(x, sp[I]);
       }
+#endif
       if (hasQ) {
         float g[2][4];
 #pragma unroll
@@ -392,6 +398,7 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
 #pragma unroll
             for (int c = 0; c < 4; ++c) sq[I] += cur[I][h][c] * g[h][c];
       }
+#if QMFX_WBS_SPLIT
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
 #pragma unroll
@@ -400,6 +407,21 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
           acc[t] = mma_split6(sp[I], sp[J], acc[t]);
         }
       }
+#else
+      // exact fp32 products on the f32 matrix path: the j-th of a lane's 8 columns is
+      // the K index of MFMA j (K = the lane group's column 32s + 8g + j), no split VALU
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            const int t = tile_index(I, J);
+            acc[t] = M::mma(cur[I][j >> 2][j & 3], cur[J][j >> 2][j & 3], acc[t]);
+          }
+        }
+      }
+#endif
       if (s + 1 < NS) {
 #pragma unroll
         for (int I = 0; I < NTN; ++I) {
