@@ -566,6 +566,229 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// Whitened row kernel, streamed, fp64 (k = 80..128): the fp32 streamed kernel's plan on the
+// fp64 matrix path.  K = Zₛ Zₛᵀ accumulates over 16-column chunks of the gathered rows with
+// the next chunk in flight: lane (i, g) holds columns 16s + 4g .. +3 of signal 16I + i, and
+// its j-th value is the K index of 16x16x4 f64 MFMA j (exact fp64 products, no split).
+// x' = Zₛᵀu gathers the rows a second time after the solve.  Replaces the multi-wave kernel
+// whose register-resident Zₛ (half a row of doubles per lane) spilled.
+// ---------------------------------------------------------------------------------------
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+template <int NTK, int NTN>
+__global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
+  using M = Mfma<double>;
+  using acc_t = typename M::acc_t;
+  constexpr int KP = 16 * NTK;
+  constexpr int NTT = NTN * (NTN + 1) / 2;
+  constexpr int NS = NTK;  // 16-column chunks
+  __shared__ __attribute__((aligned(16))) CholShared<double, NTN> S;
+  __shared__ __attribute__((aligned(16))) double gq[16 * NTN];
+
+  const int lane = threadIdx.x;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
+  const int64_t row = dn.row;
+  const int n = dn.n;  // ≤ 16·NTN by bucketing
+  const bool mine = lane < n;
+  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
+  const double vr = mine ? a.val[dn.beg + lane] : 0.0;
+  const double wl = mine ? a.alpha * vr : 0.0;
+  const double cwl = mine ? 1.0 + a.alpha * vr : 0.0;
+  const bool isP = mine && wl > 0.0;
+  const bool isQ = mine && wl == 0.0;
+  int bad = __any(mine && wl < 0.0) ? 1 : 0;
+  const uint64_t mQ = __ballot(isQ);
+  const bool hasQ = mQ != 0;
+
+  // this lane's signals 16I + cl (padding signals read the all-zero row a.zrow)
+  const f64x2* zp[NTN];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int ce = __shfl(cr, 16 * I + cl, 64);
+    zp[I] = reinterpret_cast<const f64x2*>(a.Y + (uint64_t)(uint32_t)ce * KP);
+  }
+  auto load_chunk = [&](int s, double (&buf)[NTN][4]) {
+    const int c2 = 8 * s + 2 * kk;  // f64x2 index of column 16s + 4kk
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const f64x2 u = zp[I][c2], v = zp[I][c2 + 1];
+      buf[I][0] = u[0], buf[I][1] = u[1], buf[I][2] = v[0], buf[I][3] = v[1];
+    }
+  };
+
+  acc_t acc[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0.0, 0.0, 0.0, 0.0};
+  double sq[NTN];  // z_eᵀ Σ_{f∈Q} z_f over this lane's columns (rows with Q signals)
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) sq[I] = 0.0;
+  {
+    double cur[NTN][4], nxt[NTN][4];
+    load_chunk(0, cur);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      if (hasQ) {
+        double g[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double v = 0.0;
+#pragma unroll
+          for (int I = 0; I < NTN; ++I)
+            if ((mQ >> (16 * I + cl)) & 1) v += cur[I][c];
+          g[c] = v;
+        }
+        row16_sum4(g);
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) sq[I] += cur[I][c] * g[c];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            const int t = tile_index(I, J);
+            acc[t] = M::mma(cur[I][j], cur[J][j], acc[t]);
+          }
+        }
+      }
+      if (s + 1 < NS) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) cur[I][c] = nxt[I][c];
+      }
+      // one chunk and the next chunk's loads live at a time
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  double xb = 0.0;
+  double ul[NTN], cv[NTN];
+  if (!hasQ) {
+    const double iw = isP ? 1.0 / wl : 1.0;
+    const double rhs = isP ? cwl * iw : 0.0;
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const double iwd = __shfl(iw, 16 * I + cl, 64);
+      const int t = tile_index(I, I);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : 0.0;
+    }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    __syncthreads();
+    chol_solve<double, NTN>(acc, S, lane, bad);
+    const double ue = lane < 16 * NTN ? S.xs[lane] : 0.0;
+    xb = wave_sum(isP ? rhs * (cwl - ue) : 0.0);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      ul[I] = S.xs[16 * I + cl];
+      cv[I] = 0.0;
+    }
+  } else {
+    double rhs = isP ? cwl / wl : 0.0;
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      double v = sq[I];
+      v += shfl_xor(v, 16);
+      v += shfl_xor(v, 32);
+      if (kk == 0) gq[16 * I + cl] = v;
+    }
+    __syncthreads();
+    const double kqv = lane < 16 * NTN ? gq[lane] : 0.0;
+    if (isP) rhs -= kqv;
+    const double iw = isP ? 1.0 / wl : 0.0;
+    const uint64_t mP = __ballot(isP);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const double iwd = __shfl(iw, 16 * I + cl, 64);
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        const int f = 16 * J + cl;
+        const bool pf = (mP >> f) & 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = 16 * I + M::crow(lane, r);
+          const bool pe = (mP >> e) & 1;
+          double v = acc[t][r];
+          if (pe && pf) v += (e == f) ? iwd : 0.0;
+          else v = (e == f) ? 1.0 : 0.0;
+          acc[t][r] = v;
+        }
+      }
+    }
+    if (lane < 16 * NTN) S.bw[lane] = rhs;
+    __syncthreads();
+    chol_solve<double, NTN>(acc, S, lane, bad);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const int e = 16 * I + cl;
+      const bool pe = (mP >> e) & 1;
+      const bool qe = (mQ >> e) & 1;
+      ul[I] = pe ? S.xs[e] : (qe ? 1.0 : 0.0);
+      cv[I] = __shfl(cwl, e, 64);
+    }
+  }
+
+  // x' = Zₛᵀu (and for rows with Q signals xᵀb = x'ᵀ(Zₛᵀc)), the rows gathered again
+  {
+    double cur[NTN][4], nxt[NTN][4];
+    load_chunk(0, cur);
+    double xbq = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      double sx[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double v = 0.0;
+#pragma unroll
+        for (int I = 0; I < NTN; ++I) v += cur[I][c] * ul[I];
+        sx[c] = v;
+      }
+      row16_sum4(sx);
+      if (hasQ) {
+        double sb[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double v = 0.0;
+#pragma unroll
+          for (int I = 0; I < NTN; ++I) v += cur[I][c] * cv[I];
+          sb[c] = v;
+        }
+        row16_sum4(sb);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xbq += sx[c] * sb[c];
+      }
+      // lanes cl = 0, 1 of each 16-lane row store columns 16s + 4kk + 2cl .. +1
+      if (cl < 2) {
+        f64x2 o = cl == 0 ? f64x2{sx[0], sx[1]} : f64x2{sx[2], sx[3]};
+        if (bad) o = f64x2{0.0, 0.0};
+        reinterpret_cast<f64x2*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
+      }
+      if (s + 1 < NS) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) cur[I][c] = nxt[I][c];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
+  }
+  const double csum = wave_sum(cwl);
+  if (lane == 0) {
+    a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
+    if (bad && a.status) a.status[row] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Whitened row kernel, multi-wave: the same n×n solve as wals_woodbury_kernel for factor
 // counts whose whitened rows do not fit one wave's registers (fp64 k > 64, fp32 k = 256).
 // One workgroup of NWK waves per row; wave w holds the column blocks q = w·KW .. w·KW+KW-1
@@ -1056,6 +1279,34 @@ static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStre
 #undef QMFX_WBMW
 }
 
+// fp64 k = 80..128: the streamed kernel (QMFX_WB_ST64=0: the multi-wave kernel)
+static bool wb_st64() {
+  const char* e = std::getenv("QMFX_WB_ST64");
+  return !e || std::atoi(e) != 0;
+}
+template <int NTK>
+static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, hipStream_t s) {
+  if (a.nrows <= 0) return hipSuccess;
+  if (!a.desc) return hipErrorInvalidValue;
+#define QMFX_WBS64(N)                                                                      \
+  return launch_row_chunks(a, 64, [&](const SolveArgs<double>& c) {                        \
+    hipLaunchKernelGGL((wals_woodbury_st64_kernel<NTK, N>), dim3((unsigned)c.nrows), dim3(64), \
+                       0, s, c);                                                           \
+  })
+  switch (ntn) {
+    case 1: QMFX_WBS64(1);
+    case 2: QMFX_WBS64(2);
+    case 3:
+      if constexpr (NTK >= 6) QMFX_WBS64(3);
+      return hipErrorInvalidValue;
+    case 4:
+      if constexpr (NTK >= 8) QMFX_WBS64(4);
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+#undef QMFX_WBS64
+}
+
 // fp32 k = 256: the multi-wave kernel, or the one-wave one with QMFX_WB_MW=0
 static bool wb_mw_fp32() {
   const char* e = std::getenv("QMFX_WB_MW");
@@ -1154,7 +1405,17 @@ hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipS
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
-  // one wave up to k = 64; k = 80..128 on the multi-wave kernel
+  // one wave up to k = 64; k = 80..128 on the streamed kernel (QMFX_WB_ST64=0: the
+  // multi-wave one)
+  if (nt >= 5 && nt <= 8 && wb_st64()) {
+    switch (nt) {
+      case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
+      case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
+      case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);
+      case 8: return launch_woodbury_st64_ntk<8>(a, ntn, s);
+      default: break;
+    }
+  }
   switch (nt) {
     case 5: return launch_woodbury_mw_ntk<double, 5>(a, ntn, s);
     case 6: return launch_woodbury_mw_ntk<double, 6>(a, ntn, s);

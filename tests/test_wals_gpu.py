@@ -230,11 +230,16 @@ def test_row_system_matches_oracle():
     (32, 64, 30000, "0"),
     # multi-wave whitened kernel: fp64 k = 80..128, fp32 k = 256 with QMFX_WB_MW=1; the
     # 160K-signal sets put users at ~40 signals (every n×n bucket up to n = 64)
+    # fp64 k = 80..128 run the streamed fp64 kernel; "st64=0" forces the multi-wave one
     (128, 64, 30000, "0"), (128, 64, 160000, "0"), (80, 64, 160000, "0"), (112, 64, 160000, "0"),
+    (128, 64, 160000, "st64=0"), (80, 64, 30000, "st64=0"),
     (256, 32, 160000, "1"), (256, 32, 30000, "1")])
 def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
+    if mw.startswith("st64="):
+        monkeypatch.setenv("QMFX_WB_ST64", mw[5:])
+        mw = "0"
     monkeypatch.setenv("QMFX_WB_MW", mw)
     u, i, v = synth(4000, 900, nnz, seed=11)  # ~7.5 (or ~40) signals per user
     v[::7] = 0.0  # zero-valued signals (Q set: c = 1, w = 0)
