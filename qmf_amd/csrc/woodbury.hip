@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(256) void chol_inv_kernel(const T* G, int k, double
 
 
 #ifndef QMFX_KERNELS_ONLY
-// fp32 k ≤ 128: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
+// fp32 k ≤ 128 and k = 256: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
 static bool wb_stream() {
   const char* e = std::getenv("QMFX_WB_STREAM");
   return !e || std::atoi(e) != 0;
@@ -1193,7 +1193,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
-  if constexpr (sizeof(T) == 4 && NTK <= 8) {
+  if constexpr (sizeof(T) == 4 && (NTK <= 8 || NTK == 16)) {
     if (!a.trace && wb_stream()) {
 #define QMFX_WBS(N)                                                                        \
   return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                             \
@@ -1307,10 +1307,11 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
 #undef QMFX_WBS64
 }
 
-// fp32 k = 256: the multi-wave kernel, or the one-wave one with QMFX_WB_MW=0
+// fp32 k = 256: the streamed one-wave kernel (C5 user half 161 -> 152 ms), or the
+// multi-wave kernel with QMFX_WB_MW=1
 static bool wb_mw_fp32() {
   const char* e = std::getenv("QMFX_WB_MW");
-  return !e || std::atoi(e) != 0;
+  return e && std::atoi(e) != 0;
 }
 
 template <typename T, int NT>
