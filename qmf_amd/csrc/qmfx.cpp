@@ -869,7 +869,7 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     c->trace_cap = L.n_ord;
   }
   if (trace_path) HIPCHK(hipMemsetAsync(c->trace, 0, (size_t)L.n_ord * 64, c->stream));
-  const bool dist = c->comm && c->world > 1;
+  const bool dist = c->comm != nullptr;
   const int P = (int)L.pieces.size();
   int64_t nD = 0;
   for (int j = 0; j < P; ++j) {
@@ -1450,7 +1450,9 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
   if (set_dev(c)) return -2;
   c->rank = rank;
   c->world = world;
-  if (world > 1 && id128) {
+  // world = 1 with an id: a one-rank communicator, so a single GPU runs the RCCL calls of
+  // the half (the self-broadcasts and the loss all-reduce) — the tests' loopback check
+  if (id128) {
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));

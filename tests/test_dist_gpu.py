@@ -52,3 +52,32 @@ def test_partitioned_ranks_assemble_the_full_half(k, precision, world):
             c.set_factors(side, full)
     for c in ranks:
         c.close()
+
+
+@pytest.mark.parametrize("k,precision,pieces", [(16, 64, "1"), (128, 32, "1"), (128, 32, "4")])
+def test_rccl_loopback_matches_plain(k, precision, pieces, monkeypatch):
+    """One rank with a real RCCL communicator (qmfx_dist_init(0, 1, id)): every half runs
+    the grouped per-piece ncclBroadcasts on the collective stream and the loss
+    ncclAllReduce, and must give bit-for-bit the factors and loss of a context without a
+    communicator — the RCCL path's init, stream and event ordering on real hardware."""
+    monkeypatch.setenv("QMFX_PIECES", pieces)  # 4: the broadcasts overlap the next piece
+    u, i, v = synth(3000, 600, 60000, seed=5)
+    uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
+    init = np.random.default_rng(4).uniform(-0.01, 0.01, (len(iids), k))
+    ctxs = []
+    for uid in (None, qmf_amd.rccl_unique_id()):
+        c = qmf_amd.Context(k, precision)
+        c.set_shape(len(uids), len(iids))
+        c.upload_csr(0, *ucsr)
+        c.upload_csr(1, *icsr)
+        c.set_factors(1, init)
+        if uid is not None:
+            c.dist_init(0, 1, uid)
+        ctxs.append(c)
+    for _ in range(2):
+        for side in (0, 1):
+            l0, l1 = (c.wals_half(side, ALPHA, LAM) for c in ctxs)
+            assert l0 == l1, side
+            assert np.array_equal(ctxs[0].factors(side), ctxs[1].factors(side)), side
+    for c in ctxs:
+        c.close()
