@@ -72,6 +72,11 @@ hipError_t launch_gram_big(const float* Y, int64_t n, int nt, float* G, double* 
                            int max_blocks, hipStream_t s);
 hipError_t launch_gram_big(const double* Y, int64_t n, int nt, double* G, double* partial,
                            int max_blocks, hipStream_t s);
+// whitened-row buckets: n ≤ 16·NTN, NTN = 1..kMaxNTN (NTN > 4 only for fp32 k = 256)
+constexpr int kMaxNTN = 8;
+// largest whitened bucket at fp32 k = 256: 8 on the streamed kernel, 4 on the multi-wave
+// (QMFX_WB_MW=1) or register-resident (QMFX_WB_STREAM=0) ones
+int whitened_max_ntn_k256();
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,

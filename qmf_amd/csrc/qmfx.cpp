@@ -59,12 +59,12 @@ struct SideBuf {
   int64_t shard_off = 0;
   bool sharded = false;
   std::vector<int64_t> bounds;          // per-rank row boundaries (world+1)
-  // Row buckets of this rank (device list `order`): [whitened n≤16 | ≤32 | ≤48 | ≤64 |
-  // direct rows, heaviest first].  wb[i]..wb[i+1] = whitened bucket NTN = i+1; wb[4]..n_ord
-  // = direct.  nnz per bucket class for the roofline accounting.
+  // Row buckets of this rank (device list `order`): [whitened n≤16 | ≤32 | … | ≤16·kMaxNTN |
+  // direct rows, heaviest first].  wb[i]..wb[i+1] = whitened bucket NTN = i+1;
+  // wb[kMaxNTN]..n_ord = direct.  nnz per bucket class for the roofline accounting.
   int64_t* d_order = nullptr;
   RowDesc* d_desc = nullptr;  // per slot of d_order: CSR range and row
-  int64_t wb[5] = {0, 0, 0, 0, 0};
+  int64_t wb[kMaxNTN + 1] = {};
   int64_t n_ord = 0;
   double nnz_w = 0, nnz_d = 0;
   double flops_w = 0;  // algorithmic flops of the whitened rows per half (see qmfx_wals_half)
@@ -74,7 +74,7 @@ struct SideBuf {
   // several ranks, piece j of every rank is all-gathered while piece j+1 is solved.
   struct Piece {
     int64_t rb = 0, re = 0, ord = 0, n_ord = 0;
-    int64_t wb[5] = {0, 0, 0, 0, 0};
+    int64_t wb[kMaxNTN + 1] = {};
   };
   std::vector<Piece> pieces;
   std::vector<int64_t> pbounds;  // world × (npieces + 1): piece boundaries of every rank
@@ -270,7 +270,9 @@ int max_whitened_ntn(const qmfx_ctx* c) {
   // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) and fp64
   // k = 80..128 (NT = 5..8, the multi-wave whitened kernel)
   if (use_big(c)) {
-    if (c->prec == 32) return c->nt == 16 ? 4 : 0;
+    // fp32 k = 256: the streamed kernel takes n ≤ 128 (two signals per lane past 64), the
+    // multi-wave one (QMFX_WB_MW=1) n ≤ 64
+    if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256() : 0;
     return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
   }
   int m = c->nt / 2;
@@ -331,7 +333,7 @@ int build_buckets(qmfx_ctx* c, int side) {
     pc.rb = sb.pbounds[(size_t)c->rank * (P + 1) + j];
     pc.re = sb.pbounds[(size_t)c->rank * (P + 1) + j + 1];
     pc.ord = (int64_t)order.size();
-    std::vector<int64_t> wlist[4];
+    std::vector<int64_t> wlist[kMaxNTN];
     std::vector<std::pair<int64_t, int64_t>> direct;
     for (int64_t r = pc.rb; r < pc.re; ++r) {
       const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
@@ -349,17 +351,17 @@ int build_buckets(qmfx_ctx* c, int side) {
     }
     std::stable_sort(direct.begin(), direct.end(),
                      [](const auto& x, const auto& y) { return x.first > y.first; });
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kMaxNTN; ++i) {
       pc.wb[i] = (int64_t)order.size() - pc.ord;
       order.insert(order.end(), wlist[i].begin(), wlist[i].end());
     }
-    pc.wb[4] = (int64_t)order.size() - pc.ord;
-    nw_total += pc.wb[4];
+    pc.wb[kMaxNTN] = (int64_t)order.size() - pc.ord;
+    nw_total += pc.wb[kMaxNTN];
     for (const auto& d : direct) order.push_back(d.second);
     pc.n_ord = (int64_t)order.size() - pc.ord;
   }
-  for (int i = 0; i < 4; ++i) sb.wb[i] = 0;
-  sb.wb[4] = nw_total;  // whitened rows of this rank (all pieces)
+  for (int i = 0; i < kMaxNTN; ++i) sb.wb[i] = 0;
+  sb.wb[kMaxNTN] = nw_total;  // whitened rows of this rank (all pieces)
   sb.n_ord = (int64_t)order.size();
   sb.nnz_w = nnz_w;
   sb.nnz_d = nnz_d;
@@ -814,7 +816,7 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   if (int rc = ensure_side_factors(c, 1 - side)) return rc;
   if (int rc = ensure_rowloss(c, L.n)) return rc;
   const int64_t rb = L.rbeg, re = L.rend, nrows = re - rb;
-  const int64_t nW = L.wb[4];                   // whitened rows (buckets 0..3)
+  const int64_t nW = L.wb[kMaxNTN];             // whitened rows (all buckets)
   const bool use_w = nW > 0 && lambda > 0.0;    // M = YᵀY + λI is SPD only for λ > 0
   const bool fp32 = c->prec == 32;
   HIPCHK(hipEventRecord(c->evh[0], c->stream));
@@ -875,7 +877,7 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   for (int j = 0; j < P; ++j) {
     const SideBuf::Piece& pc = L.pieces[j];
     // direct rows (heaviest first); all rows when the whitened form is off
-    const int64_t d0 = pc.ord + (use_w ? pc.wb[4] : 0);
+    const int64_t d0 = pc.ord + (use_w ? pc.wb[kMaxNTN] : 0);
     const int64_t nd = pc.ord + pc.n_ord - d0;
     nD += nd;
     HIPCHK(hipEventRecord(c->evp[j][0], c->stream));
@@ -899,8 +901,8 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
     }
     HIPCHK(hipEventRecord(c->evp[j][1], c->stream));
     // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
-    if (use_w && pc.wb[4] > 0) {
-      for (int b = 0; b < 4; ++b) {
+    if (use_w && pc.wb[kMaxNTN] > 0) {
+      for (int b = 0; b < kMaxNTN; ++b) {
         const int64_t cnt = pc.wb[b + 1] - pc.wb[b];
         if (cnt <= 0) continue;
         if (fp32) {
@@ -918,10 +920,10 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
         }
       }
       if (fp32)
-        HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order + pc.ord, pc.wb[4], c->nt,
+        HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN], c->nt,
                              (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
       else
-        HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[4],
+        HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN],
                              c->nt, (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
     }
     // rows the Cholesky kernels flagged: pivoted fp64 re-solve before the all-gather

@@ -304,8 +304,14 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 #ifndef QMFX_WBS_SPLIT
 #define QMFX_WBS_SPLIT 1
 #endif
+// n×n buckets beyond 64 signals (NTN = 5..8, k = 256): each lane carries H = 2 signals (e
+// = lane and lane + 64); the registers of the wider tiles leave two or one waves per SIMD.
+template <int NTN>
+constexpr int wb_st_waves() {
+  return NTN <= 4 ? QMFX_WB_ST_WAVES : (NTN == 5 ? 2 : 1);
+}
 template <int NTK, int NTN>
-__global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(SolveArgs<float> a) {
+__global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kernel(SolveArgs<float> a) {
   using M = Mfma<float>;
   using acc_t = f32x4;
   constexpr int KP = 16 * NTK;
@@ -314,28 +320,41 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
   __shared__ __attribute__((aligned(16))) CholShared<float, NTN> S;
   __shared__ __attribute__((aligned(16))) float gq[16 * NTN];
 
+  constexpr int H = NTN > 4 ? 2 : 1;  // signals per lane: e = lane + 64h
   const int lane = threadIdx.x;
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
   const int64_t row = dn.row;
   const int n = dn.n;  // ≤ 16·NTN by bucketing
-  const bool mine = lane < n;
-  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
-  const float vr = mine ? a.val[dn.beg + lane] : 0.f;
-  const float wl = mine ? a.alpha * vr : 0.f;
-  const float cwl = mine ? 1.f + a.alpha * vr : 0.f;
-  const bool isP = mine && wl > 0.f;
-  const bool isQ = mine && wl == 0.f;
-  int bad = __any(mine && wl < 0.f) ? 1 : 0;
-  const uint64_t mQ = __ballot(isQ);
-  const bool hasQ = mQ != 0;
+  bool mine[H], isP[H], isQ[H];
+  int cr[H];
+  float wl[H], cwl[H];
+  uint64_t mQ[H];
+  int bad = 0;
+  bool hasQ = false;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int e = lane + 64 * h;
+    mine[h] = e < n;
+    cr[h] = mine[h] ? a.col[dn.beg + e] : a.zrow;
+    const float vr = mine[h] ? a.val[dn.beg + e] : 0.f;
+    wl[h] = mine[h] ? a.alpha * vr : 0.f;
+    cwl[h] = mine[h] ? 1.f + a.alpha * vr : 0.f;
+    isP[h] = mine[h] && wl[h] > 0.f;
+    isQ[h] = mine[h] && wl[h] == 0.f;
+    bad |= __any(mine[h] && wl[h] < 0.f) ? 1 : 0;
+    mQ[h] = __ballot(isQ[h]);
+    hasQ |= mQ[h] != 0;
+  }
+  // bit e of a per-signal mask held as H 64-bit words
+  auto bit = [](const uint64_t (&m)[H], int e) -> bool { return (m[e >> 6] >> (e & 63)) & 1; };
 
   // this lane's signals 16I + cl (padding signals read the all-zero row a.zrow)
   const f32x4* zp[NTN];
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
-    const int ce = __shfl(cr, 16 * I + cl, 64);
+    const int ce = __shfl(cr[I >> 2], (16 * I + cl) & 63, 64);
     zp[I] = reinterpret_cast<const f32x4*>(a.Y + (uint64_t)(uint32_t)ce * KP);
   }
   auto load_chunk = [&](int s, f32x4 (&buf)[NTN][2]) {
@@ -386,7 +405,7 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
             float v = 0.f;
 #pragma unroll
             for (int I = 0; I < NTN; ++I)
-              if ((mQ >> (16 * I + cl)) & 1) v += cur[I][h][c];
+              if (bit(mQ, 16 * I + cl)) v += cur[I][h][c];
             g[h][c] = v;
           }
         row16_sum4(g[0]);
@@ -437,27 +456,40 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
   double xb = 0.0;
   float ul[NTN], cv[NTN];
   if (!hasQ) {
-    const float iw = isP ? fast_rcp(wl) : 1.f;
-    const float rhs = isP ? cwl * iw : 0.f;
+    float iw[H], rhs[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      iw[h] = isP[h] ? fast_rcp(wl[h]) : 1.f;
+      rhs[h] = isP[h] ? cwl[h] * iw[h] : 0.f;
+    }
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      const float iwd = __shfl(iw, 16 * I + cl, 64);
+      const float iwd = __shfl(iw[I >> 2], (16 * I + cl) & 63, 64);
       const int t = tile_index(I, I);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : 0.f;
     }
-    if (lane < 16 * NTN) S.bw[lane] = rhs;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     chol_solve<float, NTN>(acc, S, lane, bad);
-    const float ue = lane < 16 * NTN ? S.xs[lane] : 0.f;
-    xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
+    double xbl = 0.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float ue = lane + 64 * h < 16 * NTN ? S.xs[lane + 64 * h] : 0.f;
+      xbl += isP[h] ? (double)(rhs[h] * (cwl[h] - ue)) : 0.0;
+    }
+    xb = wave_sum(xbl);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       ul[I] = S.xs[16 * I + cl];
       cv[I] = 0.f;
     }
   } else {
-    float rhs = isP ? cwl * fast_rcp(wl) : 0.f;
+    float rhs[H], iw[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) rhs[h] = isP[h] ? cwl[h] * fast_rcp(wl[h]) : 0.f;
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       float v = sq[I];
@@ -466,22 +498,26 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
       if (kk == 0) gq[16 * I + cl] = v;
     }
     __syncthreads();
-    const float kqv = lane < 16 * NTN ? gq[lane] : 0.f;
-    if (isP) rhs -= kqv;
-    const float iw = isP ? fast_rcp(wl) : 0.f;
-    const uint64_t mP = __ballot(isP);
+    uint64_t mP[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float kqv = lane + 64 * h < 16 * NTN ? gq[lane + 64 * h] : 0.f;
+      if (isP[h]) rhs[h] -= kqv;
+      iw[h] = isP[h] ? fast_rcp(wl[h]) : 0.f;
+      mP[h] = __ballot(isP[h]);
+    }
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      const float iwd = __shfl(iw, 16 * I + cl, 64);
+      const float iwd = __shfl(iw[I >> 2], (16 * I + cl) & 63, 64);
 #pragma unroll
       for (int J = 0; J <= I; ++J) {
         const int t = tile_index(I, J);
         const int f = 16 * J + cl;
-        const bool pf = (mP >> f) & 1;
+        const bool pf = bit(mP, f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int e = 16 * I + M::crow(lane, r);
-          const bool pe = (mP >> e) & 1;
+          const bool pe = bit(mP, e);
           float v = acc[t][r];
           if (pe && pf) v += (e == f) ? iwd : 0.f;
           else v = (e == f) ? 1.f : 0.f;
@@ -489,16 +525,18 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
         }
       }
     }
-    if (lane < 16 * NTN) S.bw[lane] = rhs;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     chol_solve<float, NTN>(acc, S, lane, bad);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       const int e = 16 * I + cl;
-      const bool pe = (mP >> e) & 1;
-      const bool qe = (mQ >> e) & 1;
+      const bool pe = bit(mP, e);
+      const bool qe = bit(mQ, e);
       ul[I] = pe ? S.xs[e] : (qe ? 1.f : 0.f);
-      cv[I] = __shfl(cwl, e, 64);
+      cv[I] = __shfl(cwl[I >> 2], e & 63, 64);
     }
   }
 
@@ -558,7 +596,10 @@ __global__ __launch_bounds__(64, QMFX_WB_ST_WAVES) void wals_woodbury_st_kernel(
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
   }
-  const double csum = wave_sum((double)cwl);
+  double cs = 0.0;
+#pragma unroll
+  for (int h = 0; h < H; ++h) cs += (double)cwl[h];
+  const double csum = wave_sum(cs);
   if (lane == 0) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
     if (bad && a.status) a.status[row] = 1;
@@ -1210,6 +1251,19 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
         case 4:
           if constexpr (NTK >= 8) QMFX_WBS(4);
           return hipErrorInvalidValue;
+        // n = 65..128 (two signals per lane): fp32 k = 256 only
+        case 5:
+          if constexpr (NTK == 16) QMFX_WBS(5);
+          return hipErrorInvalidValue;
+        case 6:
+          if constexpr (NTK == 16) QMFX_WBS(6);
+          return hipErrorInvalidValue;
+        case 7:
+          if constexpr (NTK == 16) QMFX_WBS(7);
+          return hipErrorInvalidValue;
+        case 8:
+          if constexpr (NTK == 16) QMFX_WBS(8);
+          return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
       }
 #undef QMFX_WBS
@@ -1312,6 +1366,11 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
 static bool wb_mw_fp32() {
   const char* e = std::getenv("QMFX_WB_MW");
   return e && std::atoi(e) != 0;
+}
+int whitened_max_ntn_k256() {
+  if (!wb_stream() || wb_mw_fp32()) return 4;
+  const char* e = std::getenv("QMFX_WB_K256_NTN");  // comparisons: 4 keeps n > 64 direct
+  return e ? std::min(std::max(std::atoi(e), 1), 8) : 8;
 }
 
 template <typename T, int NT>
