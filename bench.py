@@ -212,6 +212,7 @@ CLASS_KERNELS = {
     "wals_direct_kernel": ("wals_direct_kernel<",),
     "wals_big_kernel": ("wals_big_kernel<",),
     "wals_whitened (row solve + unwhiten)": ("wals_woodbury_kernel<", "wals_woodbury_mw_kernel<",
+                                             "wals_woodbury_st_kernel<", "wals_woodbury_st64_kernel<",
                                              "whiten_kernel<{T}, {NT}, true>"),
     "bpr_epoch_kernel": ("bpr_epoch_kernel<",),
 }

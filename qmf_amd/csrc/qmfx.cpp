@@ -246,8 +246,9 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
   return hipStreamSynchronize(c->stream);
 }
 
-// Largest whitened-row bucket (NTN) usable for this factor tiling: n padded to 16 must be
-// at most 64 and at most KP/2 (beyond that the k×k solve is the cheaper one).
+// Largest whitened-row bucket (NTN) usable for this factor tiling: n padded to 16 at most
+// KP/2 and 64, except fp32 k = 128 / 256 on the streamed kernel (two signals per lane): n ≤
+// 128 (the n×n system stays the smaller one up to n ≈ k; measured at C3 and C5).
 // Factor counts beyond one wave's registers (fp32 k > 128, fp64 k > 64) use the multi-wave
 // row kernel and the tiled YᵀY (wals_big.hip).
 // YᵀY on the tiled multi-wave kernel (fp32 k > 128, fp64 k > 64)
@@ -278,6 +279,7 @@ int max_whitened_ntn(const qmfx_ctx* c) {
   int m = c->nt / 2;
   if (m > 4) m = 4;
   if (c->prec == 64 && m > 2) m = 2;
+  if (c->prec == 32 && c->nt == 8) m = whitened_max_ntn_k128();
   return m;
 }
 

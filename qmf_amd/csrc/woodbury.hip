@@ -1251,18 +1251,18 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
         case 4:
           if constexpr (NTK >= 8) QMFX_WBS(4);
           return hipErrorInvalidValue;
-        // n = 65..128 (two signals per lane): fp32 k = 256 only
+        // n = 65..128 (two signals per lane): fp32 k = 128 and 256
         case 5:
-          if constexpr (NTK == 16) QMFX_WBS(5);
+          if constexpr (NTK == 16 || NTK == 8) QMFX_WBS(5);
           return hipErrorInvalidValue;
         case 6:
-          if constexpr (NTK == 16) QMFX_WBS(6);
+          if constexpr (NTK == 16 || NTK == 8) QMFX_WBS(6);
           return hipErrorInvalidValue;
         case 7:
-          if constexpr (NTK == 16) QMFX_WBS(7);
+          if constexpr (NTK == 16 || NTK == 8) QMFX_WBS(7);
           return hipErrorInvalidValue;
         case 8:
-          if constexpr (NTK == 16) QMFX_WBS(8);
+          if constexpr (NTK == 16 || NTK == 8) QMFX_WBS(8);
           return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
       }
@@ -1366,6 +1366,13 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
 static bool wb_mw_fp32() {
   const char* e = std::getenv("QMFX_WB_MW");
   return e && std::atoi(e) != 0;
+}
+// largest whitened bucket at fp32 k = 128: n ≤ 128 on the streamed kernel (same-box A/B at
+// C3: 163.6 -> 158.7 ms/epoch over keeping n > 64 direct; QMFX_WB_K128_NTN=4 restores that)
+int whitened_max_ntn_k128() {
+  if (!wb_stream()) return 4;
+  const char* e = std::getenv("QMFX_WB_K128_NTN");
+  return e ? std::min(std::max(std::atoi(e), 1), 8) : 8;
 }
 int whitened_max_ntn_k256() {
   if (!wb_stream() || wb_mw_fp32()) return 4;
