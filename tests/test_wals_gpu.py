@@ -234,8 +234,9 @@ def test_row_system_matches_oracle():
     (128, 64, 30000, "0"), (128, 64, 160000, "0"), (80, 64, 160000, "0"), (112, 64, 160000, "0"),
     (128, 64, 160000, "st64=0"), (80, 64, 30000, "st64=0"),
     (256, 32, 160000, "1"), (256, 32, 30000, "1"),
-    # fp32 k = 256, ~100 signals per user: the n = 65..128 buckets (two signals per lane)
-    (256, 32, 400000, "0")])
+    # fp32 k = 256 / 128, ~100 signals per user: the n = 65..128 buckets (two signals per
+    # lane)
+    (256, 32, 400000, "0"), (128, 32, 400000, "0")])
 def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
