@@ -1,0 +1,8 @@
+#!/bin/bash
+# fp64 k = 128 whitened n = 65..80: tests, then C3 fp64 A/B (QMFX_WB_F64_NTN=4 keeps them direct)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/ab
+timeout -k 10 700 python -u -m pytest tests/test_wals_gpu.py tests/test_configs_gpu.py tests/test_dist_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/ab/f64w.test.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/ab/f64w.test.log; exit 1; }
+tail -1 gpurun_out/ab/f64w.test.log
+CFG=c3 PREC=64 STEPS=2 bash tools/ab_env.sh "QMFX_WB_F64_NTN=4" "QMFX_WB_F64_NTN=5" "QMFX_WB_F64_NTN=4" "QMFX_WB_F64_NTN=5"
