@@ -78,6 +78,7 @@ constexpr int kMaxNTN = 8;
 // (QMFX_WB_MW=1) or register-resident (QMFX_WB_STREAM=0) ones
 int whitened_max_ntn_k256();
 int whitened_max_ntn_k128();
+int whitened_max_ntn_f64_k128();
 hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,

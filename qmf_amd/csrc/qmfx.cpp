@@ -274,6 +274,7 @@ int max_whitened_ntn(const qmfx_ctx* c) {
     // fp32 k = 256: the streamed kernel takes n ≤ 128 (two signals per lane past 64), the
     // multi-wave one (QMFX_WB_MW=1) n ≤ 64
     if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256() : 0;
+    if (c->nt == 8) return whitened_max_ntn_f64_k128();
     return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
   }
   int m = c->nt / 2;

@@ -616,7 +616,7 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 // ---------------------------------------------------------------------------------------
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <int NTK, int NTN>
-__global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
+__global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
   using M = Mfma<double>;
   using acc_t = typename M::acc_t;
   constexpr int KP = 16 * NTK;
@@ -625,28 +625,40 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
   __shared__ __attribute__((aligned(16))) CholShared<double, NTN> S;
   __shared__ __attribute__((aligned(16))) double gq[16 * NTN];
 
+  constexpr int H = NTN > 4 ? 2 : 1;  // signals per lane: e = lane + 64h
   const int lane = threadIdx.x;
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
   const int64_t row = dn.row;
   const int n = dn.n;  // ≤ 16·NTN by bucketing
-  const bool mine = lane < n;
-  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
-  const double vr = mine ? a.val[dn.beg + lane] : 0.0;
-  const double wl = mine ? a.alpha * vr : 0.0;
-  const double cwl = mine ? 1.0 + a.alpha * vr : 0.0;
-  const bool isP = mine && wl > 0.0;
-  const bool isQ = mine && wl == 0.0;
-  int bad = __any(mine && wl < 0.0) ? 1 : 0;
-  const uint64_t mQ = __ballot(isQ);
-  const bool hasQ = mQ != 0;
+  bool mine[H], isP[H], isQ[H];
+  int cr[H];
+  double wl[H], cwl[H];
+  uint64_t mQ[H];
+  int bad = 0;
+  bool hasQ = false;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int e = lane + 64 * h;
+    mine[h] = e < n;
+    cr[h] = mine[h] ? a.col[dn.beg + e] : a.zrow;
+    const double vr = mine[h] ? a.val[dn.beg + e] : 0.0;
+    wl[h] = mine[h] ? a.alpha * vr : 0.0;
+    cwl[h] = mine[h] ? 1.0 + a.alpha * vr : 0.0;
+    isP[h] = mine[h] && wl[h] > 0.0;
+    isQ[h] = mine[h] && wl[h] == 0.0;
+    bad |= __any(mine[h] && wl[h] < 0.0) ? 1 : 0;
+    mQ[h] = __ballot(isQ[h]);
+    hasQ |= mQ[h] != 0;
+  }
+  auto bit = [](const uint64_t (&m)[H], int e) -> bool { return (m[e >> 6] >> (e & 63)) & 1; };
 
   // this lane's signals 16I + cl (padding signals read the all-zero row a.zrow)
   const f64x2* zp[NTN];
 #pragma unroll
   for (int I = 0; I < NTN; ++I) {
-    const int ce = __shfl(cr, 16 * I + cl, 64);
+    const int ce = __shfl(cr[I >> 2], (16 * I + cl) & 63, 64);
     zp[I] = reinterpret_cast<const f64x2*>(a.Y + (uint64_t)(uint32_t)ce * KP);
   }
   auto load_chunk = [&](int s, double (&buf)[NTN][4]) {
@@ -677,7 +689,7 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
           double v = 0.0;
 #pragma unroll
           for (int I = 0; I < NTN; ++I)
-            if ((mQ >> (16 * I + cl)) & 1) v += cur[I][c];
+            if (bit(mQ, 16 * I + cl)) v += cur[I][c];
           g[c] = v;
         }
         row16_sum4(g);
@@ -711,27 +723,40 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
   double xb = 0.0;
   double ul[NTN], cv[NTN];
   if (!hasQ) {
-    const double iw = isP ? 1.0 / wl : 1.0;
-    const double rhs = isP ? cwl * iw : 0.0;
+    double iw[H], rhs[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      iw[h] = isP[h] ? 1.0 / wl[h] : 1.0;
+      rhs[h] = isP[h] ? cwl[h] * iw[h] : 0.0;
+    }
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      const double iwd = __shfl(iw, 16 * I + cl, 64);
+      const double iwd = __shfl(iw[I >> 2], (16 * I + cl) & 63, 64);
       const int t = tile_index(I, I);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : 0.0;
     }
-    if (lane < 16 * NTN) S.bw[lane] = rhs;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     chol_solve<double, NTN>(acc, S, lane, bad);
-    const double ue = lane < 16 * NTN ? S.xs[lane] : 0.0;
-    xb = wave_sum(isP ? rhs * (cwl - ue) : 0.0);
+    double xbl = 0.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const double ue = lane + 64 * h < 16 * NTN ? S.xs[lane + 64 * h] : 0.0;
+      xbl += isP[h] ? rhs[h] * (cwl[h] - ue) : 0.0;
+    }
+    xb = wave_sum(xbl);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       ul[I] = S.xs[16 * I + cl];
       cv[I] = 0.0;
     }
   } else {
-    double rhs = isP ? cwl / wl : 0.0;
+    double rhs[H], iw[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) rhs[h] = isP[h] ? cwl[h] / wl[h] : 0.0;
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       double v = sq[I];
@@ -740,22 +765,26 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
       if (kk == 0) gq[16 * I + cl] = v;
     }
     __syncthreads();
-    const double kqv = lane < 16 * NTN ? gq[lane] : 0.0;
-    if (isP) rhs -= kqv;
-    const double iw = isP ? 1.0 / wl : 0.0;
-    const uint64_t mP = __ballot(isP);
+    uint64_t mP[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const double kqv = lane + 64 * h < 16 * NTN ? gq[lane + 64 * h] : 0.0;
+      if (isP[h]) rhs[h] -= kqv;
+      iw[h] = isP[h] ? 1.0 / wl[h] : 0.0;
+      mP[h] = __ballot(isP[h]);
+    }
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
-      const double iwd = __shfl(iw, 16 * I + cl, 64);
+      const double iwd = __shfl(iw[I >> 2], (16 * I + cl) & 63, 64);
 #pragma unroll
       for (int J = 0; J <= I; ++J) {
         const int t = tile_index(I, J);
         const int f = 16 * J + cl;
-        const bool pf = (mP >> f) & 1;
+        const bool pf = bit(mP, f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int e = 16 * I + M::crow(lane, r);
-          const bool pe = (mP >> e) & 1;
+          const bool pe = bit(mP, e);
           double v = acc[t][r];
           if (pe && pf) v += (e == f) ? iwd : 0.0;
           else v = (e == f) ? 1.0 : 0.0;
@@ -763,16 +792,18 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
         }
       }
     }
-    if (lane < 16 * NTN) S.bw[lane] = rhs;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     chol_solve<double, NTN>(acc, S, lane, bad);
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       const int e = 16 * I + cl;
-      const bool pe = (mP >> e) & 1;
-      const bool qe = (mQ >> e) & 1;
+      const bool pe = bit(mP, e);
+      const bool qe = bit(mQ, e);
       ul[I] = pe ? S.xs[e] : (qe ? 1.0 : 0.0);
-      cv[I] = __shfl(cwl, e, 64);
+      cv[I] = __shfl(cwl[I >> 2], e & 63, 64);
     }
   }
 
@@ -822,7 +853,10 @@ __global__ __launch_bounds__(64, 2) void wals_woodbury_st64_kernel(SolveArgs<dou
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
   }
-  const double csum = wave_sum(cwl);
+  double cs = 0.0;
+#pragma unroll
+  for (int h = 0; h < H; ++h) cs += cwl[h];
+  const double csum = wave_sum(cs);
   if (lane == 0) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
     if (bad && a.status) a.status[row] = 1;
@@ -1356,6 +1390,10 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
     case 4:
       if constexpr (NTK >= 8) QMFX_WBS64(4);
       return hipErrorInvalidValue;
+    // n = 65..80 (two signals per lane) at k = 128 (n > 80 spills: direct)
+    case 5:
+      if constexpr (NTK == 8) QMFX_WBS64(5);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 #undef QMFX_WBS64
@@ -1373,6 +1411,13 @@ int whitened_max_ntn_k128() {
   if (!wb_stream()) return 4;
   const char* e = std::getenv("QMFX_WB_K128_NTN");
   return e ? std::min(std::max(std::atoi(e), 1), 8) : 8;
+}
+// largest whitened bucket at fp64 k = 128: n ≤ 80 on the streamed kernel (QMFX_WB_F64_NTN=4
+// keeps n > 64 direct)
+int whitened_max_ntn_f64_k128() {
+  if (!wb_st64()) return 4;
+  const char* e = std::getenv("QMFX_WB_F64_NTN");
+  return e ? std::min(std::max(std::atoi(e), 1), 5) : 5;
 }
 int whitened_max_ntn_k256() {
   if (!wb_stream() || wb_mw_fp32()) return 4;
