@@ -3,10 +3,22 @@ k=128, with the achieved roofline fraction of the dominant kernel).
 
 A "step" is one WALS epoch (user half + item half, WALSEngine::optimize's loop body,
 WALSEngine.cpp:82-96) over a synthetic interaction matrix resident in HBM.  Default
-workload: BASELINE configs[2] (10M users × 1M items, 500M nnz, k=128, fp32) — the largest
-k=128 configuration, which fits one GPU.  With --gpus N (launched by torch.distributed.run)
-the same matrix is split over N GPUs by nnz-balanced row ranges and each half ends with an
-RCCL all-gather of the solved factors (strong scaling: total work fixed).
+workload: BASELINE configs[2] (10M users × 1M items, 500M nnz, k=128) at the reference's
+precision, fp64 (qmf/Types.h:24; the drop-in CLIs default to it too) — the largest k=128
+configuration, which fits one GPU.  `--config c3z` is the same shape with Zipf(1.0) item
+popularity (SURVEY.md §8(d) skew variant: power-law rows of up to ~10M signals).
+
+`--gpus N` runs N ranks: without a torch.distributed launcher in the environment it
+re-launches itself under `torch.distributed.run` as a child process (before anything touches
+the GPU); each rank then takes one GPU, the matrix is split over the ranks by nnz-balanced
+row ranges and each half ends with an RCCL all-gather of the solved factors (strong
+scaling: total work fixed).  A rank count that does not match --gpus, or more ranks than
+visible GPUs, fails with a non-zero exit.
+
+The CPU baseline (rank 0, N=1) is one full epoch of the reference-structure port on the box's
+CPU share (BASELINE.md CPU-baseline plan: "C3 and C5: time >= 1 full epoch"); when the time
+guard predicts that the epoch would not finish inside the run's time limit it falls back to
+the sampled estimate and says so.
 
 Prints ONE JSON line on rank 0.
 """
@@ -30,7 +42,11 @@ CONFIGS = {
     "c5": (10_000_000, 1_000_000, 500_000_000, 256, 3),
     # BPR: C2's matrix, k=64, 3 negatives, lr 0.05, no biases
     "c4": (1_000_000, 100_000, 50_000_000, 64, 2),
+    # C3 with Zipf(1.0) item popularity: 550M draws -> ~502M unique pairs; ~2400 items hold
+    # more than 16K signals (the largest ~9.4M), ~690K items at most 128
+    "c3z": (10_000_000, 1_000_000, 550_000_000, 128, 3),
 }
+ZIPF = {"c3z": 1.0}
 BPR_CONFIGS = {"c4"}
 LAM, ALPHA = 0.05, 40.0
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md
@@ -142,8 +158,8 @@ def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
 
 def cpu_epoch(ctx, cfg, nthreads):
     """One FULL epoch of the reference-structure port (both halves, serial YᵀY, every row)
-    on this matrix from the device's current item factors.  Minutes at C3: opt-in
-    (--cpu-baseline epoch)."""
+    on this matrix from the device's current item factors (the default baseline; minutes at
+    C3, so main() runs it under a time guard)."""
     po, lapack = oracle_lib()
     nu, ni, _, k, _ = cfg
     t0 = time.perf_counter()
@@ -341,41 +357,104 @@ def bench_bpr(args, rank, world):
         print(json.dumps(out), flush=True)
 
 
+T_START = time.time()
+# seconds of the whole bench process the guarded CPU epoch may run into (the driver's limit
+# is 600 s; the GPU part, the parity check and the sampled fallback come first)
+TIME_LIMIT_S = float(os.environ.get("QMFX_BENCH_LIMIT_S", "540"))
+
+# reference-structure port, one thread, measured in the survey container (SURVEY.md
+# Appendix B): Gram per signal and dsysv_ per row, µs, by k
+_GRAM_US = {30: 0.146, 64: 0.591, 128: 2.285, 256: 9.212}
+_SOLVE_US = {30: 4.3, 64: 13.57, 128: 158.45, 256: 1407.3}
+
+
+def cpu_epoch_estimate_s(nu, ni, nnz, k, nthreads):
+    """Conservative wall-time model of one port epoch (both halves' rows over `nthreads`, the
+    serial YᵀY at ≈1 ns per FMA): C3 on 16 threads → 431 s (measured 355.5 s)."""
+    kk = min(_GRAM_US, key=lambda x: abs(x - k))
+    g = _GRAM_US[kk] * (k / kk) ** 2
+    sv = _SOLVE_US[kk] * (k / kk) ** 3
+    rows = (2 * nnz * g + (nu + ni) * sv) * 1e-6 / max(nthreads, 1)
+    return rows + (nu + ni) * k * k * 1e-9
+
+
+def launch_plan(gpus, env, argv, port=None):
+    """None when this process is a rank (or the run is single-GPU); otherwise the child
+    command that runs `gpus` ranks under torch.distributed.run (one rank per GPU)."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    if port is None:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node=%d" % gpus, "--master-addr", "127.0.0.1",
+            "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, world, visible=None, local=0):
+    """Raises SystemExit unless the launcher started exactly `gpus` ranks and this rank's
+    GPU exists."""
+    if world != gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d rank(s)" % (gpus, world))
+    if visible is not None and local >= visible:
+        raise SystemExit("bench.py: --gpus %d needs %d GPUs; rank %d sees only %d"
+                         % (gpus, gpus, local, visible))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--precision", type=int, default=64, choices=(32, 64))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-baseline", default="sample", choices=("sample", "epoch", "none"))
+    ap.add_argument("--cpu-baseline", default="epoch", choices=("sample", "epoch", "none"))
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
     if args.no_cpu_baseline:
         args.cpu_baseline = "none"
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
 
-    import qmf_amd
-
-    cpu_share()
-    if args.config in BPR_CONFIGS:
-        # BPR shards nothing (Hogwild across GPUs would need cross-device atomics): every
-        # rank runs an independent replica; rank 0 reports
-        return bench_bpr(args, int(os.environ.get("RANK", "0")), 1)
+    # N ranks: relaunch under torch.distributed.run as a CHILD process before anything
+    # touches the GPU (this process never initialises HIP), and exit with its status
+    cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:
+        log("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+        import subprocess
+        sys.exit(subprocess.run(cmd).returncode)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args.gpus, world)
+
+    import qmf_amd
+
+    check_world(args.gpus, world, qmf_amd.device_count(), local)
+    cpu_share()
+    if args.config in BPR_CONFIGS:
+        # BPR shards nothing (Hogwild across GPUs would need cross-device atomics): every
+        # rank runs an independent replica; rank 0 reports
+        return bench_bpr(args, rank, 1)
+
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
     nu, ni, nnz_req, k, seed = CONFIGS[args.config]
+    zipf = ZIPF.get(args.config, 0.0)
 
     t0 = time.time()
     ctx = qmf_amd.Context(k, args.precision, device=local)
-    nnz = ctx.gen_synthetic(nu, ni, nnz_req, seed)
+    if zipf:
+        nnz = ctx.gen_synthetic_zipf(nu, ni, nnz_req, seed, zipf)
+    else:
+        nnz = ctx.gen_synthetic(nu, ni, nnz_req, seed)
     ctx.fill_uniform(1, 0.01, seed + 100)
     if world > 1:
         uid = [qmf_amd.rccl_unique_id() if rank == 0 else None]
@@ -406,7 +485,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
         dist.barrier()
-    st = ctx.solve_stats()
     ms_epoch = el / args.steps * 1e3
     solves = (nu + ni) * args.steps
     value = solves / el
@@ -455,7 +533,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32" if args.precision == 32 else "f64",
-        "data": "synthetic (device-generated uniform unique pairs, w in 1..5, seed %d)" % seed,
+        "data": ("synthetic (device-generated: uniform users, Zipf(%g) item popularity, w in "
+                 "1..5, seed %d)" % (zipf, seed)) if zipf else
+                "synthetic (device-generated uniform unique pairs, w in 1..5, seed %d)" % seed,
         "config": {"workload": "%s: %d users x %d items, %d nnz, k=%d, lambda=%g, alpha=%g"
                    % (args.config, nu, ni, nnz, k, LAM, ALPHA),
                    "nusers": nu, "nitems": ni, "nnz": nnz, "nfactors": k,
@@ -470,19 +550,51 @@ def main():
         out["parity"] = parity_check(ctx, CONFIGS[args.config], nthreads)
         log("parity check %.1fs: %s" % (time.perf_counter() - t0, out["parity"]))
     if args.cpu_baseline != "none" and world == 1:
+        cfg = (nu, ni, nnz, k, seed)
+
+        def baseline(tcpu, sample, detail):
+            detail["host"] = host
+            return {"value": round((nu + ni) / tcpu, 1), "unit": "solves/s", "cores": nthreads,
+                    "kind": "port", "ms_per_epoch": round(tcpu * 1e3, 1), "sample": sample,
+                    "detail": detail}
+
+        def sampled(budget):
+            tcpu, detail = cpu_baseline(ctx, CONFIGS[args.config], nthreads, budget)
+            return baseline(tcpu, "strided row samples of each half of this matrix and YtY on "
+                                  "a row subset, scaled to one epoch = %.1f s" % tcpu, detail)
+
         if args.cpu_baseline == "epoch":
-            tcpu, detail = cpu_epoch(ctx, CONFIGS[args.config], nthreads)
-            sample = ("one full epoch (user half + item half, every row, serial YtY) of the "
-                      "reference-structure port on this matrix: %.1f s" % tcpu)
+            est = cpu_epoch_estimate_s(nu, ni, nnz, k, nthreads)
+            left = TIME_LIMIT_S - (time.time() - T_START)
+            log("cpu baseline: one full epoch, estimated %.0f s on %d threads; %.0f s left of "
+                "the %.0f s time guard" % (est, nthreads, left, TIME_LIMIT_S))
+            if est > left - 30:
+                out["cpu_baseline"] = sampled(args.cpu_budget)
+                out["cpu_baseline"]["sample"] += (" (the time guard skipped the full epoch: "
+                                                  "estimated %.0f s, %.0f s left)" % (est, left))
+            else:
+                # fallback first, so the guard below always has a baseline to report
+                fb = sampled(min(args.cpu_budget, 10.0))
+                fb["sample"] += " (the time guard stopped the full epoch)"
+                out["cpu_baseline"] = fb
+                import threading
+
+                def guard():  # the port runs minutes inside one ctypes call (GIL released)
+                    rest = TIME_LIMIT_S - (time.time() - T_START)
+                    if not finished.wait(max(rest, 1.0)):
+                        log("cpu baseline: time guard hit, reporting the sampled estimate")
+                        print(json.dumps(out), flush=True)
+                        os._exit(0)
+                finished = threading.Event()
+                threading.Thread(target=guard, daemon=True).start()
+                tcpu, detail = cpu_epoch(ctx, cfg, nthreads)
+                finished.set()
+                detail["sampled_estimate_s"] = round(fb["ms_per_epoch"] / 1e3, 1)
+                out["cpu_baseline"] = baseline(
+                    tcpu, "one full epoch (user half + item half, every row, serial YtY) of "
+                          "the reference-structure port on this matrix: %.1f s" % tcpu, detail)
         else:
-            tcpu, detail = cpu_baseline(ctx, CONFIGS[args.config], nthreads, args.cpu_budget)
-            sample = ("strided row samples of each half of this matrix and YtY on a row "
-                      "subset, scaled to one epoch = %.1f s (a full epoch: --cpu-baseline "
-                      "epoch)" % tcpu)
-        detail["host"] = host
-        out["cpu_baseline"] = {"value": round((nu + ni) / tcpu, 1), "unit": "solves/s",
-                               "cores": nthreads, "kind": "port", "ms_per_epoch": round(tcpu * 1e3, 1),
-                               "sample": sample, "detail": detail}
+            out["cpu_baseline"] = sampled(args.cpu_budget)
     print(json.dumps(out), flush=True)
 
 

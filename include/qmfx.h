@@ -71,6 +71,11 @@ int qmfx_get_ids(qmfx_ctx* ctx, int side, int64_t* ids);
  * w in 1..5, both orientations built on the device.  *nnz_out = unique pairs kept. */
 int qmfx_gen_synthetic(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t nnz,
                        uint64_t seed, int64_t* nnz_out);
+/* Skewed variant (SURVEY.md §8(d) "Zipf(s=1.0) item popularity", power-law rows): `ndraws`
+ * (user uniform, item rank ~ continuous Zipf(zipf_s)) draws, duplicates dropped; zipf_s = 0
+ * is qmfx_gen_synthetic.  *nnz_out = unique pairs kept. */
+int qmfx_gen_synthetic_zipf(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t ndraws,
+                            uint64_t seed, double zipf_s, int64_t* nnz_out);
 /* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data). */
 int qmfx_download_csr(qmfx_ctx* ctx, int side, int64_t* rowptr, int32_t* colidx,
                       float* values);
@@ -94,6 +99,11 @@ int qmfx_wals_half(qmfx_ctx* ctx, int side, double alpha, double lambda, double*
  * the half's all-gather, and failed with -6 if one was exactly singular (CHECK(info == 0),
  * Matrix.cpp:94). */
 int qmfx_wals_failed_rows(qmfx_ctx* ctx, int64_t* rows, int64_t cap, int64_t* count);
+/* The row plan of `side` on this rank (11 counts): [0..7] whitened rows in the n×n buckets
+ * n ≤ 16·(i+1) (used when λ > 0), [8] direct k×k rows, [9] split-K heavy rows (more than
+ * QMFX_HEAVY_MIN signals, default 16384; the one-wave direct tilings, k ≤ 128), [10] their
+ * segments (QMFX_SEG_LEN signals each, default 8192). */
+int qmfx_row_classes(qmfx_ctx* ctx, int side, int64_t* counts);
 /* Per-row loss terms of the last half (n_side values; the sum is *loss_sum). */
 int qmfx_wals_row_losses(qmfx_ctx* ctx, double* out);
 /* One row's system as the reference forms it (updateFactorsForOne, WALSEngine.cpp:266-299),
@@ -145,6 +155,16 @@ int qmfx_rccl_unique_id(uint8_t* id128);
  * signals on the device.  id128 = NULL sets up the partition without a communicator: each
  * half then solves only this rank's rows and exchanges nothing (tests of the partition). */
 int qmfx_dist_init(qmfx_ctx* ctx, int rank, int world, const uint8_t* id128);
+/* One process driving n GPUs (the drop-in C++ engine's --ngpus): ctxs[i] (each on its own
+ * device, all with the same data and factors) become ranks 0..n-1 of one RCCL clique
+ * (ncclCommInitAll), partitioned and sharded as qmfx_dist_init does.  Fails when two
+ * contexts share a device or a device is not visible. */
+int qmfx_dist_init_all(qmfx_ctx* const* ctxs, int n);
+/* qmfx_wals_half over the n contexts of one qmfx_dist_init_all, from one thread: every
+ * context's solves are enqueued piece by piece and each piece's all-gather of all ranks is
+ * one RCCL group, overlapping the next piece's solves.  *loss_sum: the global sum. */
+int qmfx_wals_half_multi(qmfx_ctx* const* ctxs, int n, int side, double alpha, double lambda,
+                         double* loss_sum);
 /* nnz-balanced contiguous row range owned by `rank` (host-only helper, no GPU needed). */
 int qmfx_partition_rows(const int64_t* rowptr, int64_t nrows, int world, int rank,
                         int64_t* begin, int64_t* end);

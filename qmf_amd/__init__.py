@@ -7,8 +7,8 @@ The product is the C ABI in ``include/qmfx.h`` implemented by ``qmf_amd/_build/l
 GPU is present the calls fail loudly.
 """
 from ._abi import (  # noqa: F401
-    LIB_PATH, QmfxError, Context, build, dist_plan, lib, partition_rows, rccl_unique_id, selftest_mfma,
-    version,
+    LIB_PATH, QmfxError, Context, build, device_count, dist_init_all, dist_plan, lib, partition_rows, rccl_unique_id, selftest_mfma,
+    version, wals_half_multi,
 )
 
 USERS = 0

@@ -34,6 +34,7 @@ SIGNATURES = {
     "qmfx_get_shape": [vp, P_i64, P_i64, P_i64],
     "qmfx_upload_csr": [vp, c_int, P_i64, P_i32, P_f64, c_i64],
     "qmfx_gen_synthetic": [vp, c_i64, c_i64, c_i64, c_u64, P_i64],
+    "qmfx_gen_synthetic_zipf": [vp, c_i64, c_i64, c_i64, c_u64, c_dbl, P_i64],
     "qmfx_download_csr": [vp, c_int, P_i64, P_i32, P_f32],
     "qmfx_group_signals": [vp, vp, c_i64, P_i64, P_i64],
     "qmfx_get_ids": [vp, c_int, P_i64],
@@ -43,6 +44,7 @@ SIGNATURES = {
     "qmfx_wals_half": [vp, c_int, c_dbl, c_dbl, P_f64],
     "qmfx_wals_failed_rows": [vp, P_i64, c_i64, P_i64],
     "qmfx_wals_row_losses": [vp, P_f64],
+    "qmfx_row_classes": [vp, c_int, P_i64],
     "qmfx_wals_row_system": [vp, c_int, c_i64, c_dbl, c_dbl, P_f64, P_f64, P_f64],
     "qmfx_wals_set_row": [vp, c_int, c_i64, P_f64],
     "qmfx_bpr_set_positives": [vp, P_i64, P_i64, c_i64],
@@ -57,6 +59,8 @@ SIGNATURES = {
     "qmfx_dist_init": [vp, c_int, c_int, P_u8],
     "qmfx_partition_rows": [P_i64, c_i64, c_int, c_int, P_i64, P_i64],
     "qmfx_dist_plan": [P_i64, c_i64, c_int, c_int, P_i64],
+    "qmfx_dist_init_all": [ctypes.POINTER(vp), c_int],
+    "qmfx_wals_half_multi": [ctypes.POINTER(vp), c_int, c_int, c_dbl, c_dbl, P_f64],
     "qmfx_solve_kernel_stats": [vp, P_f64, P_i64, P_f64, P_f64],
     "qmfx_kernel_stats": [vp, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_reset_stats": [vp],
@@ -112,6 +116,13 @@ def selftest_mfma(precision, A, B, device=0):
     return C
 
 
+def device_count():
+    """Visible HIP devices (initialises the HIP runtime in this process)."""
+    n = c_int(0)
+    _check(lib().qmfx_device_count(ctypes.byref(n)))
+    return n.value
+
+
 def rccl_unique_id():
     buf = (ctypes.c_uint8 * 128)()
     _check(lib().qmfx_rccl_unique_id(buf))
@@ -133,6 +144,21 @@ def dist_plan(rowptr, world, npieces):
     out = np.zeros((world, npieces + 1), np.int64)
     _check(lib().qmfx_dist_plan(_p(rp, P_i64), len(rp) - 1, world, npieces, _p(out, P_i64)))
     return out
+
+
+def dist_init_all(ctxs):
+    """One process, several GPUs: the contexts (one per device, rank order) become one RCCL
+    clique (qmfx_dist_init_all)."""
+    arr = (vp * len(ctxs))(*[c.h for c in ctxs])
+    _check(lib().qmfx_dist_init_all(arr, len(ctxs)))
+
+
+def wals_half_multi(ctxs, side, alpha, lam):
+    """qmfx_wals_half over every context of one dist_init_all; returns the global loss sum."""
+    arr = (vp * len(ctxs))(*[c.h for c in ctxs])
+    out = c_dbl(0)
+    _check(lib().qmfx_wals_half_multi(arr, len(ctxs), side, alpha, lam, ctypes.byref(out)))
+    return out.value
 
 
 class Context:
@@ -180,6 +206,14 @@ class Context:
     def gen_synthetic(self, nusers, nitems, nnz, seed):
         out = c_i64(0)
         _check(lib().qmfx_gen_synthetic(self.h, nusers, nitems, nnz, seed, ctypes.byref(out)))
+        self.nusers, self.nitems = nusers, nitems
+        return out.value
+
+    def gen_synthetic_zipf(self, nusers, nitems, ndraws, seed, zipf_s):
+        """Power-law item popularity (qmfx_gen_synthetic_zipf); returns the unique nnz."""
+        out = c_i64(0)
+        _check(lib().qmfx_gen_synthetic_zipf(self.h, nusers, nitems, ndraws, seed, float(zipf_s),
+                                             ctypes.byref(out)))
         self.nusers, self.nitems = nusers, nitems
         return out.value
 
@@ -235,6 +269,13 @@ class Context:
         out = c_dbl(0)
         _check(lib().qmfx_wals_half(self.h, side, alpha, lam, ctypes.byref(out)))
         return out.value
+
+    def row_classes(self, side):
+        """Row plan of a side: {'whitened': [8 bucket counts], 'direct', 'heavy', 'segments'}."""
+        out = np.zeros(11, np.int64)
+        _check(lib().qmfx_row_classes(self.h, side, _p(out, P_i64)))
+        return {"whitened": out[:8].tolist(), "direct": int(out[8]), "heavy": int(out[9]),
+                "segments": int(out[10])}
 
     def row_losses(self, side):
         out = np.empty(self._n(side), np.float64)

@@ -20,6 +20,34 @@ __global__ void synth_keys_kernel(uint64_t* keys, int64_t n, uint64_t space, uin
   keys[i] = (uint64_t)(((unsigned __int128)h * space) >> 64);
 }
 
+// Skewed variant (SURVEY.md §8(d) "Zipf(s) item popularity"): the user is uniform, the item
+// rank r follows the continuous Zipf(s) inverse CDF on [1, nitems + 1) (s = 1:
+// P(r) = ln((r+2)/(r+1)) / ln(nitems+1)), and ranks are scattered over item ids by the
+// bijection item = (pa·r + pb) mod nitems (gcd(pa, nitems) = 1), so popular items are not
+// all at the low ids.
+__global__ void synth_keys_zipf_kernel(uint64_t* keys, int64_t n, uint64_t nusers,
+                                       uint64_t nitems, double s, uint64_t pa, uint64_t pb,
+                                       uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h1 = mix64(seed ^ mix64((uint64_t)i));
+  const uint64_t h2 = mix64(h1 ^ 0x2545f4914f6cdd1dull);
+  const uint64_t u = (uint64_t)(((unsigned __int128)h1 * nusers) >> 64);
+  const double u01 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+  const double top = (double)nitems + 1.0;
+  double x;
+  if (fabs(s - 1.0) < 1e-12) {
+    x = exp(u01 * log(top));
+  } else {
+    const double e = 1.0 - s;
+    x = pow((pow(top, e) - 1.0) * u01 + 1.0, 1.0 / e);
+  }
+  uint64_t r = x >= 1.0 ? (uint64_t)x - 1 : 0;
+  if (r >= nitems) r = nitems - 1;
+  const uint64_t it = (uint64_t)(((unsigned __int128)pa * r + pb) % nitems);
+  keys[i] = u * nitems + it;
+}
+
 __global__ void rowptr_from_keys_kernel(const uint64_t* keys, int64_t nnz, int64_t nrows,
                                         uint64_t ncols, int64_t* rowptr) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -78,6 +106,27 @@ static inline unsigned nb(int64_t n, int t = 256) { return (unsigned)((n + t - 1
 hipError_t launch_synth_keys(uint64_t* keys, int64_t n, uint64_t space, uint64_t seed,
                              hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(synth_keys_kernel, dim3(nb(n)), dim3(256), 0, s, keys, n, space, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_keys_zipf(uint64_t* keys, int64_t n, uint64_t nusers, uint64_t nitems,
+                                  double zipf_s, uint64_t seed, hipStream_t s) {
+  // a multiplier coprime to nitems near nitems·(golden ratio − 1)
+  uint64_t pa = (uint64_t)((double)nitems * 0.6180339887498949) | 1ull;
+  auto gcd = [](uint64_t a, uint64_t b) {
+    while (b) {
+      const uint64_t t = a % b;
+      a = b;
+      b = t;
+    }
+    return a;
+  };
+  if (nitems <= 1) pa = 1;
+  while (nitems > 1 && gcd(pa, nitems) != 1) pa += 2;
+  const uint64_t pb = mix64(seed ^ 0x7a1full) % (nitems ? nitems : 1);
+  if (n > 0)
+    hipLaunchKernelGGL(synth_keys_zipf_kernel, dim3(nb(n)), dim3(256), 0, s, keys, n, nusers,
+                       nitems, zipf_s, pa % (nitems ? nitems : 1), pb, seed);
   return hipGetLastError();
 }
 

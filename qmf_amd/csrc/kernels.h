@@ -37,7 +37,23 @@ struct SolveArgs {
   const T* Gimg;          // direct kernel: G + λI as per-lane accumulator tiles (gimg_kernel)
   uint64_t* trace;        // diagnostics only (QMFX_TRACE): per-slot phase timestamps
   int32_t zrow;           // whitened kernel: index of an all-zero row of Y (padding signals)
+  // Heavy rows (split-K, direct kernel only): rows with more than `heavy_min` signals are cut
+  // into segments; seg_mode 1 accumulates one segment's Gram (slot = segment) into
+  // part/partb/partc, heavy_reduce_kernel sums a row's segments in fp64 (fixed order) into
+  // its first segment's slot, and seg_mode 2 solves the row from there (desc.beg = that
+  // slot, desc.n = 0).  seg_mode 0 is the ordinary row solve.
+  int seg_mode;
+  T* part;                // [segments][NTT·256] accumulator-tile images
+  T* partb;               // [segments][KP] right-hand sides
+  double* partc;          // [segments][2]: Σc, negative-weight flag
 };
+
+// Heavy-row partial reduction: for heavy rows h0 .. h0+nh, segments hseg[h] .. hseg[h+1] are
+// summed (fp64, fixed order) with G + λI into segment hseg[h]'s slot.
+hipError_t launch_heavy_reduce(float* part, float* partb, double* partc, const int64_t* hseg,
+                               int64_t h0, int64_t nh, const float* Gimg, int nt, hipStream_t s);
+hipError_t launch_heavy_reduce(double* part, double* partb, double* partc, const int64_t* hseg,
+                               int64_t h0, int64_t nh, const double* Gimg, int nt, hipStream_t s);
 
 // Per-row kernels take one workgroup per row (slot = row_begin + blockIdx.x).  A launch's
 // total thread count must fit 32 bits (10M rows × 512 threads does not), so rows go out in
@@ -65,6 +81,9 @@ hipError_t launch_gimg(const double* G, int nt, int k, double lambda, double* im
 
 hipError_t launch_wals_direct(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_direct(const SolveArgs<double>& a, int nt, hipStream_t s);
+// seg_mode 1 / 2 of the direct kernel (wals_heavy.hip; launch_wals_direct forwards there)
+hipError_t launch_wals_heavy(const SolveArgs<float>& a, int nt, hipStream_t s);
+hipError_t launch_wals_heavy(const SolveArgs<double>& a, int nt, hipStream_t s);
 // multi-wave row solve and tiled YᵀY for large factor counts (wals_big.hip; nt 5..16)
 hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s);
 hipError_t launch_wals_big(const SolveArgs<double>& a, int nt, hipStream_t s);
@@ -74,13 +93,28 @@ hipError_t launch_gram_big(const double* Y, int64_t n, int nt, double* G, double
                            int max_blocks, hipStream_t s);
 // whitened-row buckets: n ≤ 16·NTN, NTN = 1..kMaxNTN (NTN > 4 only for fp32 k = 256)
 constexpr int kMaxNTN = 8;
+// Whitened-kernel routes (timing comparisons; the defaults are the measured best).  Read
+// from the environment ONCE per context, at qmfx_create, so the buckets a context builds
+// and the kernels it launches for them always agree.
+struct KernelSel {
+  bool wb_stream = true;  // QMFX_WB_STREAM=0: fp32 register-resident whitened kernel
+  bool wb_st64 = true;    // QMFX_WB_ST64=0: fp64 k = 80..128 multi-wave whitened kernel
+  bool wb_mw = false;     // QMFX_WB_MW=1: fp32 k = 256 multi-wave whitened kernel
+  int mw_f64_ntn4 = 2;    // QMFX_MW_F64_NTN4: waves per row of that kernel's n ≤ 64 bucket
+  int k128_ntn = 8;       // QMFX_WB_K128_NTN: largest fp32 k = 128 bucket
+  int f64_ntn = 5;        // QMFX_WB_F64_NTN: largest fp64 k = 128 bucket
+  int k256_ntn = 8;       // QMFX_WB_K256_NTN: largest fp32 k = 256 bucket
+};
+KernelSel read_kernel_sel();
 // largest whitened bucket at fp32 k = 256: 8 on the streamed kernel, 4 on the multi-wave
 // (QMFX_WB_MW=1) or register-resident (QMFX_WB_STREAM=0) ones
-int whitened_max_ntn_k256();
-int whitened_max_ntn_k128();
-int whitened_max_ntn_f64_k128();
-hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
-hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
+int whitened_max_ntn_k256(const KernelSel& ks);
+int whitened_max_ntn_k128(const KernelSel& ks);
+int whitened_max_ntn_f64_k128(const KernelSel& ks);
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, const KernelSel& ks,
+                                hipStream_t s);
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn,
+                                const KernelSel& ks, hipStream_t s);
 hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,
                          int nt, const float* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s);
@@ -170,6 +204,9 @@ hipError_t launch_bpr_eval_f64(const double* U, const double* I, const double* b
 // Synthetic data + CSR build (data.hip)
 hipError_t launch_synth_keys(uint64_t* keys, int64_t n, uint64_t space, uint64_t seed,
                              hipStream_t s);
+// uniform user, Zipf(zipf_s) item popularity (keys u·nitems + i, duplicates possible)
+hipError_t launch_synth_keys_zipf(uint64_t* keys, int64_t n, uint64_t nusers, uint64_t nitems,
+                                  double zipf_s, uint64_t seed, hipStream_t s);
 hipError_t build_csr_from_sorted_keys(const uint64_t* keys, int64_t nnz, int64_t nrows,
                                       uint64_t ncols, int64_t* rowptr, int32_t* col,
                                       hipStream_t s);

@@ -75,9 +75,18 @@ struct SideBuf {
   struct Piece {
     int64_t rb = 0, re = 0, ord = 0, n_ord = 0;
     int64_t wb[kMaxNTN + 1] = {};
+    // split-K heavy rows (the first nh direct slots): heavy indices h0 .. h0+nh, segments
+    // s0 .. s0+ns (of the side's d_seg / d_heavy / d_hseg lists)
+    int64_t nh = 0, h0 = 0, s0 = 0, ns = 0;
   };
   std::vector<Piece> pieces;
   std::vector<int64_t> pbounds;  // world × (npieces + 1): piece boundaries of every rank
+  // split-K heavy rows of this rank: per segment {CSR begin, signals, heavy index}; per heavy
+  // row {first segment, 0, row} (the seg_mode 2 solve) and the segment prefix hseg[nh+1]
+  RowDesc* d_seg = nullptr;
+  RowDesc* d_heavy = nullptr;
+  int64_t* d_hseg = nullptr;
+  int64_t nseg = 0, nheavy = 0;
 };
 
 int32_t* colp(const SideBuf& sb) { return sb.col - sb.shard_off; }
@@ -150,6 +159,24 @@ struct qmfx_ctx {
   uint64_t bpr_epochs = 0;
   int ablate = 0;  // QMFX_ABLATE (timing experiments only)
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
+  KernelSel ksel;  // whitened-kernel routes, read once at create
+  // the half-epoch in progress (qmfx_wals_half's phases)
+  struct HalfStateT {
+    int side = 0;
+    double alpha = 0, lambda = 0;
+    bool use_w = false;
+    int64_t nD = 0;
+    const char* trace_path = nullptr;
+  } hs;
+  // split-K heavy rows (one-wave direct tilings): rows with more than heavy_min signals are
+  // cut into segments of seg_len (QMFX_HEAVY_MIN / QMFX_SEG_LEN, read once at create;
+  // heavy_min 0 = off); partials [segments][NTT·256 + KP] in the context precision + Σc/flag
+  int64_t heavy_min = 16384;
+  int64_t seg_len = 8192;
+  void* part = nullptr;
+  void* partb = nullptr;
+  double* partc = nullptr;
+  int64_t part_cap = 0;  // segments
   // whitened path buffers
   void* Z = nullptr;  // whitened fixed side [max(nu, ni)][kp]
   int64_t z_cap = 0;
@@ -273,14 +300,14 @@ int max_whitened_ntn(const qmfx_ctx* c) {
   if (use_big(c)) {
     // fp32 k = 256: the streamed kernel takes n ≤ 128 (two signals per lane past 64), the
     // multi-wave one (QMFX_WB_MW=1) n ≤ 64
-    if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256() : 0;
-    if (c->nt == 8) return whitened_max_ntn_f64_k128();
+    if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256(c->ksel) : 0;
+    if (c->nt == 8) return whitened_max_ntn_f64_k128(c->ksel);
     return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
   }
   int m = c->nt / 2;
   if (m > 4) m = 4;
   if (c->prec == 64 && m > 2) m = 2;
-  if (c->prec == 32 && c->nt == 8) m = whitened_max_ntn_k128();
+  if (c->prec == 32 && c->nt == 8) m = whitened_max_ntn_k128(c->ksel);
   return m;
 }
 
@@ -331,6 +358,11 @@ int build_buckets(qmfx_ctx* c, int side) {
   order.reserve(sb.rend - sb.rbeg);
   sb.pieces.assign(P, SideBuf::Piece{});
   int64_t nw_total = 0;
+  // split-K heavy rows: only the one-wave direct tilings (the multi-wave k > 128 kernel keeps
+  // whole rows)
+  const int64_t hmin = use_big_rows(c) ? 0 : c->heavy_min;
+  std::vector<RowDesc> segs, heavy;
+  std::vector<int64_t> hseg;
   for (int j = 0; j < P; ++j) {
     SideBuf::Piece& pc = sb.pieces[j];
     pc.rb = sb.pbounds[(size_t)c->rank * (P + 1) + j];
@@ -354,6 +386,21 @@ int build_buckets(qmfx_ctx* c, int side) {
     }
     std::stable_sort(direct.begin(), direct.end(),
                      [](const auto& x, const auto& y) { return x.first > y.first; });
+    // the heaviest direct rows (n > hmin) lead the direct section; each is cut into
+    // segments of seg_len signals
+    pc.h0 = (int64_t)heavy.size();
+    pc.s0 = (int64_t)segs.size();
+    for (const auto& d : direct) {
+      if (hmin <= 0 || d.first <= hmin) break;
+      const int64_t r = d.second, beg = sb.h_rowptr[r], n = d.first;
+      hseg.push_back((int64_t)segs.size());
+      heavy.push_back(RowDesc{(int64_t)segs.size(), 0, (int32_t)r});
+      for (int64_t o = 0; o < n; o += c->seg_len)
+        segs.push_back(RowDesc{beg + o, (int32_t)std::min(c->seg_len, n - o),
+                               (int32_t)(heavy.size() - 1)});
+    }
+    pc.nh = (int64_t)heavy.size() - pc.h0;
+    pc.ns = (int64_t)segs.size() - pc.s0;
     for (int i = 0; i < kMaxNTN; ++i) {
       pc.wb[i] = (int64_t)order.size() - pc.ord;
       order.insert(order.end(), wlist[i].begin(), wlist[i].end());
@@ -382,6 +429,30 @@ int build_buckets(qmfx_ctx* c, int side) {
   sb.d_desc = nullptr;
   HIPCHK(hipMalloc(&sb.d_desc, (size_t)std::max<int64_t>(sb.n_ord, 1) * sizeof(RowDesc)));
   HIPCHK(scopy(c, sb.d_desc, desc.data(), desc.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
+  hseg.push_back((int64_t)segs.size());
+  dfree_t(sb.d_seg);
+  dfree_t(sb.d_heavy);
+  dfree_t(sb.d_hseg);
+  sb.nseg = (int64_t)segs.size();
+  sb.nheavy = (int64_t)heavy.size();
+  if (sb.nheavy > 0) {
+    HIPCHK(hipMalloc(&sb.d_seg, segs.size() * sizeof(RowDesc)));
+    HIPCHK(hipMalloc(&sb.d_heavy, heavy.size() * sizeof(RowDesc)));
+    HIPCHK(hipMalloc(&sb.d_hseg, hseg.size() * sizeof(int64_t)));
+    HIPCHK(scopy(c, sb.d_seg, segs.data(), segs.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
+    HIPCHK(scopy(c, sb.d_heavy, heavy.data(), heavy.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
+    HIPCHK(scopy(c, sb.d_hseg, hseg.data(), hseg.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (c->part_cap < sb.nseg) {
+      dfree(c->part);
+      dfree(c->partb);
+      dfree_t(c->partc);
+      const size_t ntt = (size_t)c->nt * (c->nt + 1) / 2;
+      HIPCHK(hipMalloc(&c->part, (size_t)sb.nseg * ntt * 256 * c->esz));
+      HIPCHK(hipMalloc(&c->partb, (size_t)sb.nseg * c->kp * c->esz));
+      HIPCHK(hipMalloc(&c->partc, (size_t)sb.nseg * 2 * sizeof(double)));
+      c->part_cap = sb.nseg;
+    }
+  }
   sb.buckets_valid = true;
   return 0;
 }
@@ -434,6 +505,33 @@ FallbackArgs<T> fallback_args(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, i
   return a;
 }
 
+// One launch of the direct-row kernels over `n` slots from `b`: seg_mode 0 = slots of the
+// side's order (rows), 1 = split-K segments (d_seg), 2 = split-K heavy-row solves (d_heavy).
+template <typename T>
+hipError_t launch_direct_t(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int64_t b, int64_t n,
+                           double alpha, double lambda, const char* trace_path, int mode) {
+  SolveArgs<T> a{L.rowptr, colp(L), valp<T>(L), (const T*)R.F, (const T*)c->G, (T*)L.F,
+                 c->rowloss, c->status, L.d_order, b, n, (T)alpha, (T)lambda, c->k, c->ablate,
+                 mode == 1 ? L.d_seg : mode == 2 ? L.d_heavy : L.d_desc, (const T*)c->Gimg,
+                 (trace_path && mode == 0) ? c->trace : nullptr, (int32_t)R.n};
+  a.seg_mode = mode;
+  a.part = (T*)c->part;
+  a.partb = (T*)c->partb;
+  a.partc = c->partc;
+  return use_big_rows(c) ? launch_wals_big(a, c->nt, c->stream)
+                         : launch_wals_direct(a, c->nt, c->stream);
+}
+
+int launch_direct_range(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int64_t b, int64_t n,
+                        double alpha, double lambda, const char* trace_path, int mode) {
+  if (n <= 0) return 0;
+  const hipError_t e = c->prec == 32
+                           ? launch_direct_t<float>(c, L, R, b, n, alpha, lambda, trace_path, mode)
+                           : launch_direct_t<double>(c, L, R, b, n, alpha, lambda, trace_path, mode);
+  if (e != hipSuccess) return fail(std::string("row kernel launch: ") + hipGetErrorString(e), -2);
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -462,6 +560,9 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->esz = precision == 32 ? 4 : 8;
   if (const char* ab = std::getenv("QMFX_ABLATE")) c->ablate = std::atoi(ab);
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
+  c->ksel = read_kernel_sel();
+  if (const char* hm = std::getenv("QMFX_HEAVY_MIN")) c->heavy_min = std::max<int64_t>(std::atoll(hm), 0);
+  if (const char* sl = std::getenv("QMFX_SEG_LEN")) c->seg_len = std::max<int64_t>(std::atoll(sl), 64);
   if (const char* np = std::getenv("QMFX_PIECES"))
     c->npieces = std::min(std::max(std::atoi(np), 1), QMFX_MAX_PIECES);
   hipError_t e = hipSetDevice(device);
@@ -515,7 +616,13 @@ int qmfx_destroy(qmfx_ctx* c) {
     dfree(sb.F);
     dfree_t(sb.d_order);
     dfree_t(sb.d_desc);
+    dfree_t(sb.d_seg);
+    dfree_t(sb.d_heavy);
+    dfree_t(sb.d_hseg);
   }
+  dfree(c->part);
+  dfree(c->partb);
+  dfree_t(c->partc);
   dfree(c->G);
   dfree_t(c->gpart);
   dfree_t(c->rowloss);
@@ -710,15 +817,26 @@ int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, f
 
 int qmfx_gen_synthetic(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz, uint64_t seed,
                        int64_t* nnz_out) {
+  return qmfx_gen_synthetic_zipf(c, nusers, nitems, nnz, seed, 0.0, nnz_out);
+}
+
+int qmfx_gen_synthetic_zipf(qmfx_ctx* c, int64_t nusers, int64_t nitems, int64_t nnz,
+                            uint64_t seed, double zipf_s, int64_t* nnz_out) {
   if (nnz <= 0) return fail("nnz must be positive");
+  if (zipf_s < 0.0 || !std::isfinite(zipf_s)) return fail("zipf exponent must be >= 0");
   if (int rc = qmfx_set_shape(c, nusers, nitems)) return rc;
   const uint64_t space = (uint64_t)nusers * (uint64_t)nitems;
-  if ((uint64_t)nnz > space / 2) return fail("nnz too large for the shape");
+  if (zipf_s == 0.0 && (uint64_t)nnz > space / 2) return fail("nnz too large for the shape");
+  if (nnz > 0x7fffffffll) return fail("at most 2^31-1 draws");
   int end_bit = 64 - __builtin_clzll(space);
   uint64_t *keys = nullptr, *scratch = nullptr;
   HIPCHK(hipMalloc(&keys, (size_t)nnz * 8));
   HIPCHK(hipMalloc(&scratch, (size_t)nnz * 8));
-  HIPCHK(launch_synth_keys(keys, nnz, space, seed, c->stream));
+  if (zipf_s == 0.0)
+    HIPCHK(launch_synth_keys(keys, nnz, space, seed, c->stream));
+  else
+    HIPCHK(launch_synth_keys_zipf(keys, nnz, (uint64_t)nusers, (uint64_t)nitems, zipf_s, seed,
+                                  c->stream));
   int64_t m = 0;
   HIPCHK(sort_unique_keys(keys, scratch, nnz, &m, end_bit, c->stream));
   for (int side = 0; side < 2; ++side) {
@@ -808,7 +926,16 @@ int qmfx_fill_uniform(qmfx_ctx* c, int side, double bound, uint64_t seed) {
   return 0;
 }
 
-int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* loss_sum) {
+// ---- one WALS half-epoch in phases ------------------------------------------------------
+// qmfx_wals_half runs them in order on one context; qmfx_wals_half_multi interleaves them
+// over several contexts (one process driving several GPUs) so that piece j's all-gather of
+// every context is one RCCL group while piece j+1 computes.
+}  // extern "C"
+
+namespace {
+
+// G = YᵀY, the whitening and G + λI images, status resets (no collectives)
+int half_begin(qmfx_ctx* c, int side, double alpha, double lambda) {
   if (side != 0 && side != 1) return fail("side must be 0 or 1");
   SideBuf& L = c->s[side];
   SideBuf& R = c->s[1 - side];
@@ -818,10 +945,10 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   if (int rc = ensure_side_factors(c, side)) return rc;
   if (int rc = ensure_side_factors(c, 1 - side)) return rc;
   if (int rc = ensure_rowloss(c, L.n)) return rc;
-  const int64_t rb = L.rbeg, re = L.rend, nrows = re - rb;
   const int64_t nW = L.wb[kMaxNTN];             // whitened rows (all buckets)
   const bool use_w = nW > 0 && lambda > 0.0;    // M = YᵀY + λI is SPD only for λ > 0
   const bool fp32 = c->prec == 32;
+  c->hs = qmfx_ctx::HalfStateT{side, alpha, lambda, use_w, 0, std::getenv("QMFX_TRACE")};
   HIPCHK(hipEventRecord(c->evh[0], c->stream));
   // G = YᵀY of the fixed side (full replica on every rank)
   const bool big = use_big(c);
@@ -858,8 +985,7 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
                            (const double*)c->Linv, nullptr, 0.0, false, c->stream));
     }
   }
-  const bool big_rows = use_big_rows(c);
-  if (!big_rows) {
+  if (!use_big_rows(c)) {
     if (fp32)
       HIPCHK(launch_gimg((const float*)c->G, c->nt, c->k, lambda, (float*)c->Gimg, c->stream));
     else
@@ -867,93 +993,120 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   }
   HIPCHK(hipMemsetAsync(c->status, 0, (size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t), c->stream));
   HIPCHK(hipMemsetAsync(c->fb_cnt, 0, 2 * sizeof(unsigned long long), c->stream));
-  const char* trace_path = std::getenv("QMFX_TRACE");
+  const char* trace_path = c->hs.trace_path;
   if (trace_path && c->trace_cap < L.n_ord) {
     dfree_t(c->trace);
     HIPCHK(hipMalloc(&c->trace, (size_t)L.n_ord * 64));
     c->trace_cap = L.n_ord;
   }
   if (trace_path) HIPCHK(hipMemsetAsync(c->trace, 0, (size_t)L.n_ord * 64, c->stream));
-  const bool dist = c->comm != nullptr;
-  const int P = (int)L.pieces.size();
-  int64_t nD = 0;
-  for (int j = 0; j < P; ++j) {
-    const SideBuf::Piece& pc = L.pieces[j];
-    // direct rows (heaviest first); all rows when the whitened form is off
-    const int64_t d0 = pc.ord + (use_w ? pc.wb[kMaxNTN] : 0);
-    const int64_t nd = pc.ord + pc.n_ord - d0;
-    nD += nd;
-    HIPCHK(hipEventRecord(c->evp[j][0], c->stream));
-    if (nd > 0) {
-      if (fp32) {
-        SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)R.F,
-                           (const float*)c->G, (float*)L.F, c->rowloss, c->status, L.d_order,
-                           d0, nd, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc,
-                           (const float*)c->Gimg, trace_path ? c->trace : nullptr,
-                           (int32_t)R.n};
-        HIPCHK(big_rows ? launch_wals_big(a, c->nt, c->stream)
-                        : launch_wals_direct(a, c->nt, c->stream));
-      } else {
-        SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)R.F,
-                            (const double*)c->G, (double*)L.F, c->rowloss, c->status, L.d_order,
-                            d0, nd, alpha, lambda, c->k, c->ablate, L.d_desc,
-                            (const double*)c->Gimg, nullptr, (int32_t)R.n};
-        HIPCHK(big_rows ? launch_wals_big(a, c->nt, c->stream)
-                        : launch_wals_direct(a, c->nt, c->stream));
-      }
-    }
-    HIPCHK(hipEventRecord(c->evp[j][1], c->stream));
-    // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
-    if (use_w && pc.wb[kMaxNTN] > 0) {
-      for (int b = 0; b < kMaxNTN; ++b) {
-        const int64_t cnt = pc.wb[b + 1] - pc.wb[b];
-        if (cnt <= 0) continue;
-        if (fp32) {
-          SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)c->Z, nullptr,
-                             (float*)L.F, c->rowloss, c->status, L.d_order, pc.ord + pc.wb[b],
-                             cnt, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
-                             trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
-          HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
-        } else {
-          SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)c->Z,
-                              nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
-                              pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
-                              nullptr, nullptr, (int32_t)c->z_cap};
-          HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
-        }
-      }
-      if (fp32)
-        HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN], c->nt,
-                             (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
-      else
-        HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN],
-                             c->nt, (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
-    }
-    // rows the Cholesky kernels flagged: pivoted fp64 re-solve before the all-gather
-    if (pc.n_ord > 0) {
-      if (fp32)
-        HIPCHK(launch_wals_fallback(
-            fallback_args<float>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
-      else
-        HIPCHK(launch_wals_fallback(
-            fallback_args<double>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
-    }
-    HIPCHK(hipEventRecord(c->evp[j][2], c->stream));
-    if (dist) {
-      // piece j of every rank → every rank (an all-gather-v of contiguous row ranges), on
-      // the collective stream while the next piece is solved
-      HIPCHK(hipStreamWaitEvent(c->comm_stream, c->evp[j][2], 0));
-      NCCLCHK(ncclGroupStart());
-      for (int r = 0; r < c->world; ++r) {
-        const int64_t b = L.pbounds[(size_t)r * (P + 1) + j], e = L.pbounds[(size_t)r * (P + 1) + j + 1];
-        if (e <= b) continue;
-        char* base = (char*)L.F + (size_t)b * c->kp * c->esz;
-        NCCLCHK(ncclBroadcast(base, base, (size_t)(e - b) * c->kp, nccl_type(c->prec), r, c->comm,
-                              c->comm_stream));
-      }
-      NCCLCHK(ncclGroupEnd());
-    }
+  return 0;
+}
+
+// the row solves of piece j (direct, heavy, whitened, pivoted re-solve); records evp[j][2]
+int half_piece(qmfx_ctx* c, int j) {
+  if (set_dev(c)) return -2;
+  const int side = c->hs.side;
+  const double alpha = c->hs.alpha, lambda = c->hs.lambda;
+  const bool use_w = c->hs.use_w, fp32 = c->prec == 32;
+  const char* trace_path = c->hs.trace_path;
+  SideBuf& L = c->s[side];
+  SideBuf& R = c->s[1 - side];
+  const SideBuf::Piece& pc = L.pieces[j];
+  // direct rows (heaviest first; the split-K heavy rows lead); all rows when the whitened
+  // form is off
+  const int64_t dh = pc.ord + pc.wb[kMaxNTN];
+  c->hs.nD += pc.ord + pc.n_ord - (use_w ? dh : pc.ord);
+  HIPCHK(hipEventRecord(c->evp[j][0], c->stream));
+  if (pc.nh > 0) {
+    // heavy rows: segment Grams (one wave per segment), fixed-order fp64 reduction into
+    // each row's first segment, then the row solves from those images
+    if (int rc = launch_direct_range(c, L, R, pc.s0, pc.ns, alpha, lambda, nullptr, 1))
+      return rc;
+    if (fp32)
+      HIPCHK(launch_heavy_reduce((float*)c->part, (float*)c->partb, c->partc, L.d_hseg, pc.h0,
+                                 pc.nh, (const float*)c->Gimg, c->nt, c->stream));
+    else
+      HIPCHK(launch_heavy_reduce((double*)c->part, (double*)c->partb, c->partc, L.d_hseg,
+                                 pc.h0, pc.nh, (const double*)c->Gimg, c->nt, c->stream));
+    if (int rc = launch_direct_range(c, L, R, pc.h0, pc.nh, alpha, lambda, nullptr, 2))
+      return rc;
   }
+  if (!use_w && pc.wb[kMaxNTN] > 0) {
+    if (int rc = launch_direct_range(c, L, R, pc.ord, pc.wb[kMaxNTN], alpha, lambda, trace_path, 0))
+      return rc;
+  }
+  if (int rc = launch_direct_range(c, L, R, dh + pc.nh, pc.ord + pc.n_ord - dh - pc.nh, alpha,
+                                   lambda, trace_path, 0))
+    return rc;
+  HIPCHK(hipEventRecord(c->evp[j][1], c->stream));
+  // whitened rows: per-bucket row solve, then x = L⁻ᵀ x' and −λ‖x‖²
+  if (use_w && pc.wb[kMaxNTN] > 0) {
+    for (int b = 0; b < kMaxNTN; ++b) {
+      const int64_t cnt = pc.wb[b + 1] - pc.wb[b];
+      if (cnt <= 0) continue;
+      if (fp32) {
+        SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)c->Z, nullptr,
+                           (float*)L.F, c->rowloss, c->status, L.d_order, pc.ord + pc.wb[b],
+                           cnt, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
+                           trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->ksel, c->stream));
+      } else {
+        SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)c->Z,
+                            nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
+                            pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
+                            nullptr, nullptr, (int32_t)c->z_cap};
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->ksel, c->stream));
+      }
+    }
+    if (fp32)
+      HIPCHK(launch_whiten((const float*)L.F, (float*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN], c->nt,
+                           (const float*)c->Linv, c->rowloss, lambda, true, c->stream));
+    else
+      HIPCHK(launch_whiten((const double*)L.F, (double*)L.F, L.d_order + pc.ord, pc.wb[kMaxNTN],
+                           c->nt, (const double*)c->Linv, c->rowloss, lambda, true, c->stream));
+  }
+  // rows the Cholesky kernels flagged: pivoted fp64 re-solve before the all-gather
+  if (pc.n_ord > 0) {
+    if (fp32)
+      HIPCHK(launch_wals_fallback(
+          fallback_args<float>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
+    else
+      HIPCHK(launch_wals_fallback(
+          fallback_args<double>(c, L, R, pc.ord, pc.n_ord, alpha, lambda), c->stream));
+  }
+  HIPCHK(hipEventRecord(c->evp[j][2], c->stream));
+  return 0;
+}
+
+// piece j of this rank → every rank (one ncclGroup; nests inside a caller's group)
+int half_comm_piece(qmfx_ctx* c, int j) {
+  if (set_dev(c)) return -2;
+  SideBuf& L = c->s[c->hs.side];
+  const int P = (int)L.pieces.size();
+  if (c->comm) {
+    // piece j of every rank → every rank (an all-gather-v of contiguous row ranges), on
+    // the collective stream while the next piece is solved
+    HIPCHK(hipStreamWaitEvent(c->comm_stream, c->evp[j][2], 0));
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < c->world; ++r) {
+      const int64_t b = L.pbounds[(size_t)r * (P + 1) + j], e = L.pbounds[(size_t)r * (P + 1) + j + 1];
+      if (e <= b) continue;
+      char* base = (char*)L.F + (size_t)b * c->kp * c->esz;
+      NCCLCHK(ncclBroadcast(base, base, (size_t)(e - b) * c->kp, nccl_type(c->prec), r, c->comm,
+                            c->comm_stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+  }
+  return 0;
+}
+
+// trace dump (diagnostics), the loss sum and the status block
+int half_tail(qmfx_ctx* c) {
+  if (set_dev(c)) return -2;
+  const int side = c->hs.side;
+  const char* trace_path = c->hs.trace_path;
+  SideBuf& L = c->s[side];
   if (trace_path) {
     std::vector<uint64_t> h((size_t)L.n_ord * 8);
     HIPCHK(scopy(c, h.data(), c->trace, h.size() * 8, hipMemcpyDeviceToHost));
@@ -963,18 +1116,35 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
       std::fclose(f);
     }
   }
-  HIPCHK(launch_sum_f64(c->rowloss + rb, nrows, c->dsum, c->stream));
-  if (dist) {
+  HIPCHK(launch_sum_f64(c->rowloss + L.rbeg, L.rend - L.rbeg, c->dsum, c->stream));
+  // loss, re-solve counts and the factorization flag in one status block
+  HIPCHK(launch_half_status(c->dsum, c->fb_cnt, c->hs.use_w ? c->chol_status : nullptr,
+                            c->dsum + kHalfStatus, c->stream));
+  return 0;
+}
+
+int half_comm_status(qmfx_ctx* c) {
+  if (set_dev(c)) return -2;
+  if (c->comm) {
+    // the whole status block is summed over the ranks, so every rank sees the same
+    // singular-row count and fails (-6) in the same half instead of leaving the others in
+    // the next half's collectives
     HIPCHK(hipEventRecord(c->ev_sum, c->stream));
     HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_sum, 0));
-    NCCLCHK(ncclAllReduce(c->dsum, c->dsum, 1, ncclFloat64, ncclSum, c->comm, c->comm_stream));
+    NCCLCHK(ncclAllReduce(c->dsum + kHalfStatus, c->dsum + kHalfStatus, 4, ncclFloat64, ncclSum,
+                          c->comm, c->comm_stream));
     HIPCHK(hipEventRecord(c->ev_comm, c->comm_stream));
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
   }
+  return 0;
+}
+
+int half_end(qmfx_ctx* c, double* loss_sum) {
+  if (set_dev(c)) return -2;
+  SideBuf& L = c->s[c->hs.side];
+  const int P = (int)L.pieces.size();
   HIPCHK(hipEventRecord(c->evh[2], c->stream));
-  // loss, re-solve counts and the factorization flag: one small copy into pinned memory
-  HIPCHK(launch_half_status(c->dsum, c->fb_cnt, use_w ? c->chol_status : nullptr,
-                            c->dsum + kHalfStatus, c->stream));
+  // one small copy into pinned memory
   HIPCHK(hipMemcpyAsync(c->hsum, c->dsum + kHalfStatus, 4 * sizeof(double),
                         hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -994,6 +1164,8 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   }
   HIPCHK(hipEventElapsedTime(&ms_h, c->evh[0], c->evh[2]));
   const double k = c->k, s = (double)c->esz;
+  const bool use_w = c->hs.use_w;
+  const int64_t nD = c->hs.nD, nW = L.wb[kMaxNTN];
   const double nzd = use_w ? L.nnz_d : L.nnz_d + L.nnz_w, nd = (double)nD;
   const double nzw = use_w ? L.nnz_w : 0.0, nw = use_w ? (double)nW : 0.0;
   double fl_d = 0, by_d = 0, fl_w = 0, by_w = 0;
@@ -1023,8 +1195,86 @@ int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* l
   c->solve_launches += 1;
   c->solve_flops += fl_d + fl_w;
   c->solve_bytes += by_d + by_w;
-  c->last_side = side;
+  c->last_side = c->hs.side;
   if (loss_sum) *loss_sum = *c->hsum;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qmfx_wals_half(qmfx_ctx* c, int side, double alpha, double lambda, double* loss_sum) {
+  if (int rc = half_begin(c, side, alpha, lambda)) return rc;
+  const int P = (int)c->s[side].pieces.size();
+  for (int j = 0; j < P; ++j) {
+    if (int rc = half_piece(c, j)) return rc;
+    if (int rc = half_comm_piece(c, j)) return rc;
+  }
+  if (int rc = half_tail(c)) return rc;
+  if (c->comm) {
+    NCCLCHK(ncclGroupStart());
+    const int rc = half_comm_status(c);
+    NCCLCHK(ncclGroupEnd());
+    if (rc) return rc;
+  }
+  return half_end(c, loss_sum);
+}
+
+int qmfx_wals_half_multi(qmfx_ctx* const* ctxs, int n, int side, double alpha, double lambda,
+                         double* loss_sum) {
+  if (n < 1 || !ctxs) return fail("no contexts");
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]) return fail("null context");
+    if (n > 1 && (!ctxs[i]->comm || ctxs[i]->world != n || ctxs[i]->rank != i))
+      return fail("contexts must come from one qmfx_dist_init_all, in rank order");
+  }
+  for (int i = 0; i < n; ++i)
+    if (int rc = half_begin(ctxs[i], side, alpha, lambda)) return rc;
+  const int P = (int)ctxs[0]->s[side].pieces.size();
+  for (int i = 1; i < n; ++i)
+    if ((int)ctxs[i]->s[side].pieces.size() != P) return fail("contexts disagree on the pieces");
+  for (int j = 0; j < P; ++j) {
+    for (int i = 0; i < n; ++i)
+      if (int rc = half_piece(ctxs[i], j)) return rc;
+    // one thread drives every communicator: all ranks' broadcasts of piece j in one group
+    NCCLCHK(ncclGroupStart());
+    int rc = 0;
+    for (int i = 0; i < n && rc == 0; ++i) rc = half_comm_piece(ctxs[i], j);
+    NCCLCHK(ncclGroupEnd());
+    if (rc) return rc;
+  }
+  for (int i = 0; i < n; ++i)
+    if (int rc = half_tail(ctxs[i])) return rc;
+  {
+    NCCLCHK(ncclGroupStart());
+    int rc = 0;
+    for (int i = 0; i < n && rc == 0; ++i)
+      if (ctxs[i]->comm) rc = half_comm_status(ctxs[i]);
+    NCCLCHK(ncclGroupEnd());
+    if (rc) return rc;
+  }
+  double first = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double l = 0.0;
+    if (int rc = half_end(ctxs[i], &l)) return rc;
+    if (i == 0) first = l;
+  }
+  if (loss_sum) *loss_sum = first;
+  return 0;
+}
+
+int qmfx_row_classes(qmfx_ctx* c, int side, int64_t* counts) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  const SideBuf& sb = c->s[side];
+  if (!sb.buckets_valid) return fail("row buckets not built");
+  for (int i = 0; i < kMaxNTN + 3; ++i) counts[i] = 0;
+  for (const auto& pc : sb.pieces) {
+    for (int b = 0; b < kMaxNTN; ++b) counts[b] += pc.wb[b + 1] - pc.wb[b];
+    counts[kMaxNTN] += pc.n_ord - pc.wb[kMaxNTN] - pc.nh;
+    counts[kMaxNTN + 1] += pc.nh;
+    counts[kMaxNTN + 2] += pc.ns;
+  }
   return 0;
 }
 
@@ -1450,6 +1700,25 @@ int qmfx_rccl_unique_id(uint8_t* id128) {
   return 0;
 }
 
+}  // extern "C"
+
+// This rank's row ranges of both sides, the row buckets, and (world > 1) the CSR shard.
+static int dist_partition(qmfx_ctx* c) {
+  const int rank = c->rank, world = c->world;
+  for (int side = 0; side < 2; ++side) {
+    SideBuf& sb = c->s[side];
+    if (sb.h_rowptr.empty()) continue;
+    if (sb.sharded) return fail("qmfx_dist_init: the CSR is already sharded (re-upload it first)");
+    set_default_bounds(sb, world, rank);
+    if (int rc = build_buckets(c, side)) return rc;
+    if (world > 1)
+      if (int rc = shard_csr(c, sb)) return rc;
+  }
+  return 0;
+}
+
+extern "C" {
+
 int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
   if (world < 1 || rank < 0 || rank >= world) return fail("bad rank/world");
   if (set_dev(c)) return -2;
@@ -1463,14 +1732,37 @@ int qmfx_dist_init(qmfx_ctx* c, int rank, int world, const uint8_t* id128) {
     NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
     if (!c->comm_stream) HIPCHK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   }
-  for (int side = 0; side < 2; ++side) {
-    SideBuf& sb = c->s[side];
-    if (sb.h_rowptr.empty()) continue;
-    if (sb.sharded) return fail("qmfx_dist_init: the CSR is already sharded (re-upload it first)");
-    set_default_bounds(sb, world, rank);
-    if (int rc = build_buckets(c, side)) return rc;
-    if (world > 1)
-      if (int rc = shard_csr(c, sb)) return rc;
+  return dist_partition(c);
+}
+
+int qmfx_dist_init_all(qmfx_ctx* const* ctxs, int n) {
+  if (n < 1 || !ctxs) return fail("qmfx_dist_init_all: no contexts");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  std::vector<int> devs((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]) return fail("qmfx_dist_init_all: null context");
+    if (ctxs[i]->comm) return fail("qmfx_dist_init_all: context already has a communicator");
+    devs[(size_t)i] = ctxs[i]->device;
+    for (int j = 0; j < i; ++j)
+      if (devs[(size_t)j] == devs[(size_t)i])
+        return fail("qmfx_dist_init_all: two contexts on device " + std::to_string(devs[(size_t)i]) +
+                    " (one GPU per rank)");
+    if (devs[(size_t)i] < 0 || devs[(size_t)i] >= ndev)
+      return fail("qmfx_dist_init_all: " + std::to_string(n) + " ranks need device " +
+                  std::to_string(devs[(size_t)i]) + " but only " + std::to_string(ndev) +
+                  " GPU(s) are visible");
+  }
+  std::vector<ncclComm_t> comms((size_t)n);
+  NCCLCHK(ncclCommInitAll(comms.data(), n, devs.data()));
+  for (int i = 0; i < n; ++i) {
+    qmfx_ctx* c = ctxs[i];
+    if (set_dev(c)) return -2;
+    c->comm = comms[(size_t)i];
+    c->rank = i;
+    c->world = n;
+    if (!c->comm_stream) HIPCHK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (int rc = dist_partition(c)) return rc;
   }
   return 0;
 }

@@ -1257,19 +1257,43 @@ __global__ __launch_bounds__(256) void chol_inv_kernel(const T* G, int k, double
 
 
 #ifndef QMFX_KERNELS_ONLY
-// fp32 k ≤ 128 and k = 256: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
-static bool wb_stream() {
-  const char* e = std::getenv("QMFX_WB_STREAM");
-  return !e || std::atoi(e) != 0;
+static bool env_flag(const char* name, bool dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) != 0 : dflt;
+}
+static int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* e = std::getenv(name);
+  return e ? std::min(std::max(std::atoi(e), lo), hi) : dflt;
+}
+KernelSel read_kernel_sel() {
+  KernelSel k;
+  // fp32 k ≤ 128 and k = 256: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
+  k.wb_stream = env_flag("QMFX_WB_STREAM", true);
+  // fp64 k = 80..128: the streamed kernel (QMFX_WB_ST64=0: the multi-wave kernel)
+  k.wb_st64 = env_flag("QMFX_WB_ST64", true);
+  // fp32 k = 256: the streamed one-wave kernel (C5 user half 161 -> 152 ms), or the
+  // multi-wave kernel with QMFX_WB_MW=1
+  k.wb_mw = env_flag("QMFX_WB_MW", false);
+  // fp64 n×n bucket 4 at k = 128 on the multi-wave kernel: 2 waves per row spill 76 VGPRs, 4
+  // waves do not (2 or 4, for comparisons)
+  k.mw_f64_ntn4 = env_int("QMFX_MW_F64_NTN4", QMFX_MW_F64_NTN4_DEFAULT, 2, 4);
+  // largest whitened bucket at fp32 k = 128: n ≤ 128 on the streamed kernel (same-box A/B at
+  // C3: 163.6 -> 158.7 ms/epoch over keeping n > 64 direct; 4 restores that)
+  k.k128_ntn = env_int("QMFX_WB_K128_NTN", 8, 1, 8);
+  // largest whitened bucket at fp64 k = 128: n ≤ 80 on the streamed kernel (4 keeps n > 64
+  // direct)
+  k.f64_ntn = env_int("QMFX_WB_F64_NTN", 5, 1, 5);
+  k.k256_ntn = env_int("QMFX_WB_K256_NTN", 8, 1, 8);  // comparisons: 4 keeps n > 64 direct
+  return k;
 }
 
 template <typename T, int NTK>
-static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
+static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, bool stream, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
   if constexpr (sizeof(T) == 4 && (NTK <= 8 || NTK == 16)) {
-    if (!a.trace && wb_stream()) {
+    if (!a.trace && stream) {
 #define QMFX_WBS(N)                                                                        \
   return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                             \
     hipLaunchKernelGGL((wals_woodbury_st_kernel<NTK, N>), dim3((unsigned)c.nrows), b, 0, s, c); \
@@ -1328,21 +1352,15 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
   return hipGetLastError();
 }
 
-// multi-wave whitened kernel: 4 waves per row
-// fp64 n×n bucket 4 at k = 128: 2 waves per row spill 76 VGPRs, 4 waves do not
-// (QMFX_MW_F64_NTN4 = 2 or 4 picks one for comparisons)
-static int mw_f64_ntn4_waves() {
-  const char* e = std::getenv("QMFX_MW_F64_NTN4");
-  return e ? std::atoi(e) : QMFX_MW_F64_NTN4_DEFAULT;
-}
-
+// multi-wave whitened kernel: 4 waves per row (the fp64 n ≤ 64 bucket: ntn4_waves)
 template <typename T, int NTK>
-static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
+static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, int ntn4_waves,
+                                         hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   constexpr int NWK = QMFX_MW_NWK;
   if constexpr (sizeof(T) == 8 && NTK >= 8) {
-    if (ntn == 4 && mw_f64_ntn4_waves() == 4)
+    if (ntn == 4 && ntn4_waves == 4)
       return launch_row_chunks(a, 256, [&](const SolveArgs<T>& c) {
         hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, 4, 4>), dim3((unsigned)c.nrows),
                            dim3(256), 0, s, c);
@@ -1367,11 +1385,6 @@ static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, hipStre
 #undef QMFX_WBMW
 }
 
-// fp64 k = 80..128: the streamed kernel (QMFX_WB_ST64=0: the multi-wave kernel)
-static bool wb_st64() {
-  const char* e = std::getenv("QMFX_WB_ST64");
-  return !e || std::atoi(e) != 0;
-}
 template <int NTK>
 static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
@@ -1399,30 +1412,10 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
 #undef QMFX_WBS64
 }
 
-// fp32 k = 256: the streamed one-wave kernel (C5 user half 161 -> 152 ms), or the
-// multi-wave kernel with QMFX_WB_MW=1
-static bool wb_mw_fp32() {
-  const char* e = std::getenv("QMFX_WB_MW");
-  return e && std::atoi(e) != 0;
-}
-// largest whitened bucket at fp32 k = 128: n ≤ 128 on the streamed kernel (same-box A/B at
-// C3: 163.6 -> 158.7 ms/epoch over keeping n > 64 direct; QMFX_WB_K128_NTN=4 restores that)
-int whitened_max_ntn_k128() {
-  if (!wb_stream()) return 4;
-  const char* e = std::getenv("QMFX_WB_K128_NTN");
-  return e ? std::min(std::max(std::atoi(e), 1), 8) : 8;
-}
-// largest whitened bucket at fp64 k = 128: n ≤ 80 on the streamed kernel (QMFX_WB_F64_NTN=4
-// keeps n > 64 direct)
-int whitened_max_ntn_f64_k128() {
-  if (!wb_st64()) return 4;
-  const char* e = std::getenv("QMFX_WB_F64_NTN");
-  return e ? std::min(std::max(std::atoi(e), 1), 5) : 5;
-}
-int whitened_max_ntn_k256() {
-  if (!wb_stream() || wb_mw_fp32()) return 4;
-  const char* e = std::getenv("QMFX_WB_K256_NTN");  // comparisons: 4 keeps n > 64 direct
-  return e ? std::min(std::max(std::atoi(e), 1), 8) : 8;
+int whitened_max_ntn_k128(const KernelSel& ks) { return ks.wb_stream ? ks.k128_ntn : 4; }
+int whitened_max_ntn_f64_k128(const KernelSel& ks) { return ks.wb_st64 ? ks.f64_ntn : 4; }
+int whitened_max_ntn_k256(const KernelSel& ks) {
+  return (!ks.wb_stream || ks.wb_mw) ? 4 : ks.k256_ntn;
 }
 
 template <typename T, int NT>
@@ -1510,16 +1503,18 @@ static hipError_t launch_chol_inv_nt(const T* G, int k, double lambda, T* Linv, 
   }
 }
 
-hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {
-  if (nt == 16 && wb_mw_fp32()) return launch_woodbury_mw_ntk<float, 16>(a, ntn, s);
-#define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, s)
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, const KernelSel& ks,
+                                hipStream_t s) {
+  if (nt == 16 && ks.wb_mw) return launch_woodbury_mw_ntk<float, 16>(a, ntn, ks.mw_f64_ntn4, s);
+#define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, ks.wb_stream, s)
   QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
-hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn,
+                                const KernelSel& ks, hipStream_t s) {
   // one wave up to k = 64; k = 80..128 on the streamed kernel (QMFX_WB_ST64=0: the
   // multi-wave one)
-  if (nt >= 5 && nt <= 8 && wb_st64()) {
+  if (nt >= 5 && nt <= 8 && ks.wb_st64) {
     switch (nt) {
       case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
       case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
@@ -1529,13 +1524,13 @@ hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hip
     }
   }
   switch (nt) {
-    case 5: return launch_woodbury_mw_ntk<double, 5>(a, ntn, s);
-    case 6: return launch_woodbury_mw_ntk<double, 6>(a, ntn, s);
-    case 7: return launch_woodbury_mw_ntk<double, 7>(a, ntn, s);
-    case 8: return launch_woodbury_mw_ntk<double, 8>(a, ntn, s);
+    case 5: return launch_woodbury_mw_ntk<double, 5>(a, ntn, ks.mw_f64_ntn4, s);
+    case 6: return launch_woodbury_mw_ntk<double, 6>(a, ntn, ks.mw_f64_ntn4, s);
+    case 7: return launch_woodbury_mw_ntk<double, 7>(a, ntn, ks.mw_f64_ntn4, s);
+    case 8: return launch_woodbury_mw_ntk<double, 8>(a, ntn, ks.mw_f64_ntn4, s);
     default: break;
   }
-#define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, s)
+#define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, false, s)
   QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
 }

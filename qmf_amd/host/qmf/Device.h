@@ -17,9 +17,16 @@ namespace qmf {
 // arithmetic to ~1e-12.  fp32 (opt-in) stores the factors in fp32: on well-posed problems it
 // meets the 1e-4 factor tolerance at the reference's λ/α, but its error grows as cond·6e-8,
 // so rank-deficient inputs (e.g. more factors than distinct fixed-side rows) need fp64.
+//
+// ngpus > 1 (--ngpus, QMF_NGPUS; WALS only) drives devices device .. device+ngpus-1 from this
+// process: users and items are split into nnz-balanced row ranges, one per GPU, and every
+// half-epoch ends with an RCCL all-gather of the solved rows (qmfx_dist_init_all,
+// qmfx_wals_half_multi) — the reference's scheduler/labor bucket model
+// (distributed/scheduler/RunOneTask.cpp:160-243) inside one node.
 struct DeviceOptions {
   int device = envInt("QMF_DEVICE", 0);
   int precision = envInt("QMF_PRECISION", 64);
+  int ngpus = envInt("QMF_NGPUS", 1);
 
   static int envInt(const char* name, int def) {
     const char* v = std::getenv(name);
@@ -36,10 +43,11 @@ struct DeviceOptions {
 
 class DeviceContext {
  public:
-  DeviceContext(const DeviceOptions& opt, const size_t nfactors) {
+  DeviceContext(const DeviceOptions& opt, const size_t nfactors, const int deviceOffset = 0) {
     CHECK(opt.precision == 32 || opt.precision == 64)
       << "precision must be 32 or 64, got " << opt.precision;
-    QMFX_CHECK(qmfx_create(&ctx_, opt.device, opt.precision, static_cast<int>(nfactors)));
+    QMFX_CHECK(qmfx_create(&ctx_, opt.device + deviceOffset, opt.precision,
+                           static_cast<int>(nfactors)));
   }
   ~DeviceContext() {
     if (ctx_) qmfx_destroy(ctx_);

@@ -109,6 +109,8 @@ void BPREngine::initHost(const std::vector<DatasetElem>& dataset) {
 }
 
 void BPREngine::initDevice() {
+  // Hogwild across GPUs would need cross-device atomics: BPR runs on one GPU (replicas only)
+  CHECK_EQ(deviceOptions_.ngpus, 1) << "BPR runs on one GPU (QMF_NGPUS / --ngpus is WALS only)";
   dev_ = std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors);
   qmfx_ctx* c = dev_->get();
   QMFX_CHECK(qmfx_set_shape(c, static_cast<int64_t>(nusers()), static_cast<int64_t>(nitems())));

@@ -27,7 +27,21 @@ void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
   CHECK(!userFactors_ && !itemFactors_) << "engine was already initialized with train data";
   CHECK_GT(config_.nfactors, 0);
   CHECK(!dataset.empty()) << "empty train dataset";
+  CHECK_GE(deviceOptions_.ngpus, 1) << "--ngpus must be at least 1";
+  if (deviceOptions_.ngpus > 1) {
+    int visible = 0;
+    QMFX_CHECK(qmfx_device_count(&visible));
+    CHECK_LE(deviceOptions_.device + deviceOptions_.ngpus, visible)
+        << "--ngpus " << deviceOptions_.ngpus << " from --device " << deviceOptions_.device
+        << " needs " << deviceOptions_.device + deviceOptions_.ngpus << " GPUs; " << visible
+        << " visible";
+  }
   dev_ = std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors);
+  ranks_.assign(1, dev_->get());
+  for (int r = 1; r < deviceOptions_.ngpus; ++r) {
+    peers_.push_back(std::make_unique<DeviceContext>(deviceOptions_, config_.nfactors, r));
+    ranks_.push_back(peers_.back()->get());
+  }
   qmfx_ctx* c = dev_->get();
   if (dataset.size() < static_cast<size_t>(std::numeric_limits<int32_t>::max())) {
     // ids, idx and both CSR orientations built on the device (qmfx_group_signals)
@@ -39,15 +53,22 @@ void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
     QMFX_CHECK(qmfx_get_ids(c, QMFX_ITEMS, iids.data()));
     userIndex_.assignSorted(std::move(uids));
     itemIndex_.assignSorted(std::move(iids));
+    // every rank builds the same CSR on its own device (sharded by qmfx_dist_init_all)
+    for (size_t r = 1; r < ranks_.size(); ++r)
+      QMFX_CHECK(qmfx_group_signals(ranks_[r], dataset.data(),
+                                    static_cast<int64_t>(dataset.size()), &nu, &ni));
   } else {
     // beyond the device sort's 32-bit item count: the same grouping on the host
     SignalCsr byUser, byItem;
     groupSignals(dataset, userIndex_, itemIndex_, byUser, byItem, parallel_.nthreads());
-    QMFX_CHECK(qmfx_set_shape(c, static_cast<int64_t>(nusers()), static_cast<int64_t>(nitems())));
-    QMFX_CHECK(qmfx_upload_csr(c, QMFX_USERS, byUser.rowptr.data(), byUser.col.data(),
-                               byUser.val.data(), static_cast<int64_t>(byUser.nnz())));
-    QMFX_CHECK(qmfx_upload_csr(c, QMFX_ITEMS, byItem.rowptr.data(), byItem.col.data(),
-                               byItem.val.data(), static_cast<int64_t>(byItem.nnz())));
+    for (qmfx_ctx* rc : ranks_) {
+      QMFX_CHECK(qmfx_set_shape(rc, static_cast<int64_t>(nusers()),
+                                static_cast<int64_t>(nitems())));
+      QMFX_CHECK(qmfx_upload_csr(rc, QMFX_USERS, byUser.rowptr.data(), byUser.col.data(),
+                                 byUser.val.data(), static_cast<int64_t>(byUser.nnz())));
+      QMFX_CHECK(qmfx_upload_csr(rc, QMFX_ITEMS, byItem.rowptr.data(), byItem.col.data(),
+                                 byItem.val.data(), static_cast<int64_t>(byItem.nnz())));
+    }
   }
 
   userFactors_ = std::make_unique<FactorData>(nusers(), config_.nfactors);
@@ -63,8 +84,16 @@ void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
     itemFactors_->setFactors(config_.DistributionFile);
   }
 
-  QMFX_CHECK(qmfx_set_factors(c, QMFX_USERS, userFactors_->getFactors().data()));
-  QMFX_CHECK(qmfx_set_factors(c, QMFX_ITEMS, itemFactors_->getFactors().data()));
+  for (qmfx_ctx* rc : ranks_) {
+    QMFX_CHECK(qmfx_set_factors(rc, QMFX_USERS, userFactors_->getFactors().data()));
+    QMFX_CHECK(qmfx_set_factors(rc, QMFX_ITEMS, itemFactors_->getFactors().data()));
+  }
+  if (ranks_.size() > 1) {
+    QMFX_CHECK(qmfx_dist_init_all(ranks_.data(), static_cast<int>(ranks_.size())));
+    LOG(INFO) << "rows partitioned over " << ranks_.size() << " GPUs (devices "
+              << deviceOptions_.device << ".." << deviceOptions_.device + ranks_.size() - 1
+              << "), RCCL all-gather per half-epoch";
+  }
   hostStale_ = false;
 }
 
@@ -78,7 +107,11 @@ void WALSEngine::initTest(const std::vector<DatasetElem>& testDataset) {
 
 void WALSEngine::reportFailedRows(const int side) {
   int64_t count = 0;
-  QMFX_CHECK(qmfx_wals_failed_rows(dev_->get(), nullptr, 0, &count));
+  for (qmfx_ctx* rc : ranks_) {  // each rank flags the rows it solved
+    int64_t n = 0;
+    QMFX_CHECK(qmfx_wals_failed_rows(rc, nullptr, 0, &n));
+    count += n;
+  }
   if (count == 0) return;
   // the device re-solved them in fp64 with a pivoted factorization (dsysv_'s role,
   // Matrix.cpp:81-96) inside the half; a singular one fails qmfx_wals_half itself
@@ -89,8 +122,12 @@ void WALSEngine::reportFailedRows(const int side) {
 
 Double WALSEngine::iterate(const int side) {
   Double sum = 0.0;
-  QMFX_CHECK(qmfx_wals_half(dev_->get(), side, config_.confidenceWeight,
-                            config_.regularizationLambda, &sum));
+  if (ranks_.size() > 1)
+    QMFX_CHECK(qmfx_wals_half_multi(ranks_.data(), static_cast<int>(ranks_.size()), side,
+                                    config_.confidenceWeight, config_.regularizationLambda, &sum));
+  else
+    QMFX_CHECK(qmfx_wals_half(dev_->get(), side, config_.confidenceWeight,
+                              config_.regularizationLambda, &sum));
   reportFailedRows(side);
   hostStale_ = true;
   lastLoss_ = sum / (static_cast<Double>(nusers()) * static_cast<Double>(nitems()));
@@ -105,7 +142,7 @@ void WALSEngine::optimize() {
     LOG(INFO) << "epoch " << epoch << ": train loss = " << loss;
     evaluate(epoch);
   }
-  QMFX_CHECK(qmfx_sync(dev_->get()));
+  for (qmfx_ctx* rc : ranks_) QMFX_CHECK(qmfx_sync(rc));
 }
 
 void WALSEngine::syncHost() const {

@@ -78,6 +78,10 @@ class WALSEngine : public Engine {
   DeviceOptions deviceOptions_;
   mutable ParallelExecutor parallel_;
   std::unique_ptr<DeviceContext> dev_;
+  // --ngpus > 1: the other ranks' contexts (dev_ is rank 0); all are passed to
+  // qmfx_wals_half_multi in rank order
+  std::vector<std::unique_ptr<DeviceContext>> peers_;
+  std::vector<qmfx_ctx*> ranks_;
 
   IdIndex userIndex_;
   IdIndex itemIndex_;

@@ -1,5 +1,5 @@
 // `wals` command line, drop-in for the reference's qmf/wals.cpp:26-107: same flags, same
-// log lines and output files.  Additions: --device, --precision (32 | 64).
+// log lines and output files.  Additions: --device, --precision (32 | 64), --ngpus.
 #include <memory>
 
 #include <qmf/DatasetReader.h>
@@ -21,6 +21,9 @@ DEFINE_int32(nthreads, 16, "number of host threads (ingest, evaluation, output)"
 DEFINE_int32(device, qmf::DeviceOptions::envInt("QMF_DEVICE", 0), "GPU ordinal");
 DEFINE_int32(precision, qmf::DeviceOptions::envInt("QMF_PRECISION", 64),
              "device arithmetic: 64 (fp64, the reference's Double; default) or 32 (fp32)");
+DEFINE_int32(ngpus, qmf::DeviceOptions::envInt("QMF_NGPUS", 1),
+             "GPUs to split the rows over (devices --device .. --device+ngpus-1, RCCL "
+             "all-gather per half-epoch)");
 // datasets
 DEFINE_string(train_dataset, "", "filename of training dataset");
 DEFINE_string(test_dataset, "", "filename of test dataset");
@@ -54,6 +57,7 @@ int main(int argc, char** argv) {
   qmf::DeviceOptions device;
   device.device = FLAGS_device;
   device.precision = FLAGS_precision;
+  device.ngpus = FLAGS_ngpus;
   qmf::WALSEngine engine(config, metricsEngine, static_cast<size_t>(FLAGS_nthreads), device);
 
   LOG(INFO) << "loading training data";

@@ -301,3 +301,37 @@ def test_bpr_cli_test_metrics_with_biases(tmp_path):
         vals["mse"].append(po.metric_mse(lab, S[t]))
     for name, v in vals.items():
         assert abs(float(rec["test_avg_" + name]) - np.mean(v)) < 1e-4 * max(1.0, abs(np.mean(v))), name
+
+
+def test_wals_cli_ngpus_beyond_the_visible_gpus_fails_loudly(tmp_path):
+    """--ngpus N splits the rows over N GPUs of this process (qmfx_dist_init_all); asking
+    for more GPUs than are visible aborts with the reference's CHECK convention instead of
+    quietly running on fewer."""
+    import qmf_amd
+    n = qmf_amd.device_count() + 1
+    u, i, v = load_tiny()
+    train = str(tmp_path / "train.txt")
+    write_dataset(train, u, i, v)
+    r = subprocess.run([os.path.join(BIN, "wals"), "--train_dataset=" + train, "--nepochs=1",
+                        "--nfactors=8", "--ngpus=%d" % n, "--user_factors=" + str(tmp_path / "u"),
+                        "--item_factors=" + str(tmp_path / "i")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "--ngpus %d" % n in r.stderr and "visible" in r.stderr, r.stderr[-2000:]
+
+
+def test_wals_cli_ngpus_one_is_the_plain_path(tmp_path):
+    """--ngpus 1 (the default) is the single-context path: identical files."""
+    u, i, v = load_tiny()
+    train = str(tmp_path / "train.txt")
+    write_dataset(train, u, i, v)
+    dist = str(tmp_path / "init.txt")
+    write_dist(dist, np.random.default_rng(3).uniform(-0.01, 0.01, 1000 * 8))
+    outs = []
+    for flag in ([], ["--ngpus=1"]):
+        tag = "n%d" % len(flag)
+        run("wals", "--train_dataset=" + train, "--nepochs=2", "--nfactors=8",
+            "--distribution_file=" + dist, "--user_factors=" + str(tmp_path / (tag + "u")),
+            "--item_factors=" + str(tmp_path / (tag + "i")), *flag)
+        outs.append(open(tmp_path / (tag + "u")).read() + open(tmp_path / (tag + "i")).read())
+    assert outs[0] == outs[1]

@@ -81,3 +81,69 @@ def test_rccl_loopback_matches_plain(k, precision, pieces, monkeypatch):
             assert np.array_equal(ctxs[0].factors(side), ctxs[1].factors(side)), side
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("k,precision", [(16, 64), (128, 64), (128, 32)])
+def test_multi_context_driver_matches_plain(k, precision, monkeypatch):
+    """The one-process multi-GPU driver (qmfx_dist_init_all + qmfx_wals_half_multi, the C++
+    engine's --ngpus path) on the one GPU here: a one-rank clique runs the phased half with
+    the grouped per-piece broadcasts and the status all-reduce, and must reproduce a plain
+    context bit for bit."""
+    monkeypatch.setenv("QMFX_PIECES", "3")
+    u, i, v = synth(3000, 600, 60000, seed=6)
+    uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
+    init = np.random.default_rng(5).uniform(-0.01, 0.01, (len(iids), k))
+    ctxs = []
+    for _ in range(2):
+        c = qmf_amd.Context(k, precision)
+        c.set_shape(len(uids), len(iids))
+        c.upload_csr(0, *ucsr)
+        c.upload_csr(1, *icsr)
+        c.set_factors(1, init)
+        ctxs.append(c)
+    qmf_amd.dist_init_all([ctxs[1]])
+    for _ in range(2):
+        for side in (0, 1):
+            l0 = ctxs[0].wals_half(side, ALPHA, LAM)
+            l1 = qmf_amd.wals_half_multi([ctxs[1]], side, ALPHA, LAM)
+            assert l0 == l1, side
+            assert np.array_equal(ctxs[0].factors(side), ctxs[1].factors(side)), side
+    for c in ctxs:
+        c.close()
+
+
+def test_multi_context_driver_rejects_a_shared_device():
+    """Two ranks on one GPU are refused (RCCL needs one device per rank): the drop-in CLI's
+    --ngpus 2 on a one-GPU box fails instead of silently running one rank."""
+    a, b = qmf_amd.Context(16, 64), qmf_amd.Context(16, 64)
+    for c in (a, b):
+        c.set_shape(10, 10)
+    with pytest.raises(qmf_amd.QmfxError, match="two contexts on device"):
+        qmf_amd.dist_init_all([a, b])
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("comm", ["none", "loopback", "clique"])
+def test_singular_rows_fail_every_rank(comm):
+    """An exactly singular row system (λ = 0 and an all-zero fixed side: dsysv_'s info > 0,
+    CHECK(info == 0) at Matrix.cpp:94) fails the half with -6.  With a communicator the
+    half's status block (loss, re-solved and singular counts) is all-reduced, so every rank
+    sees the count and fails in the same half."""
+    u, i, v = synth(200, 50, 1500, seed=1)
+    uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
+    c = qmf_amd.Context(8, 64)
+    c.set_shape(len(uids), len(iids))
+    c.upload_csr(0, *ucsr)
+    c.upload_csr(1, *icsr)
+    c.set_factors(1, np.zeros((len(iids), 8)))
+    if comm == "loopback":
+        c.dist_init(0, 1, qmf_amd.rccl_unique_id())
+    elif comm == "clique":
+        qmf_amd.dist_init_all([c])
+    with pytest.raises(qmf_amd.QmfxError, match="singular"):
+        if comm == "clique":
+            qmf_amd.wals_half_multi([c], 0, ALPHA, 0.0)
+        else:
+            c.wals_half(0, ALPHA, 0.0)
+    c.close()

@@ -141,3 +141,29 @@ def test_gen_uniform(tmp_path):
     assert x.shape == (1000,) and np.all(np.abs(x) <= 0.01)
     lines = open(out).read().splitlines()
     assert all(len(s.split(".")[1]) == 9 for s in lines)
+
+
+def test_cli_ngpus_without_gpus_fails_loudly(golden_dir):
+    # --ngpus 2 counts the visible GPUs first: with none (or one) it aborts, never runs on
+    # fewer ranks than asked
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is present (tests/test_cli_gpu.py covers this case there)")
+    r = subprocess.run([os.path.join(BIN, "wals"), "--train_dataset=" +
+                        os.path.join(golden_dir, "tiny.txt"), "--nepochs=1", "--nfactors=4",
+                        "--ngpus=2"], capture_output=True, text=True)
+    assert r.returncode != 0 and "qmfx_device_count" in r.stderr
+
+
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_host_unit_tests_under_sanitizers(kind):
+    """the host code (parallel parser, %.9f writer, ParallelExecutor, id
+    grouping, metrics, BPR host init) under ASan + UBSan and under TSan.  Any report fails
+    the run: ASan/UBSan abort (no recovery), TSan exits 66."""
+    exe = os.path.join(BIN, kind, "qmf_host_tests")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert " 0 failed checks" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr

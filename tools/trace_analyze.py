@@ -13,7 +13,7 @@ os.environ["QMFX_TRACE"] = path
 import qmf_amd  # noqa: E402
 
 cfg = [int(x) for x in sys.argv[1:5]] if len(sys.argv) > 4 else [10_000_000, 1_000_000, 500_000_000, 128]
-c = qmf_amd.Context(cfg[3], 32)
+c = qmf_amd.Context(cfg[3], int(os.environ.get("PREC", "32")))
 c.gen_synthetic(cfg[0], cfg[1], cfg[2], 3)
 c.fill_uniform(1, 0.01, 103)
 side = int(os.environ.get("SIDE", "0"))
