@@ -52,6 +52,7 @@ LAM, ALPHA = 0.05, 40.0
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md
 PEAK_F64_TFLOPS = 78.6
 PEAK_HBM_GBS = 8000.0
+PEAK_ATOMIC_GBS = 1300.0  # chip-wide float atomic adds (MI355X_MICROARCH.md, measured)
 
 
 def log(*a):
@@ -314,6 +315,9 @@ def bench_bpr(args, rank, world):
     upd = nnz * num_neg * args.steps
     sec = st["ms"] / 1e3 / max(st["launches"], 1)
     by = st["bytes"] / max(st["launches"], 1)
+    kp = (k + 15) // 16 * 16
+    esz = 4 if args.precision == 32 else 8
+    atomic_by = float(nnz) * (num_neg + 1) * kp * esz
     out = {
         "metric": "BPR Hogwild updates/sec at k=%d (epoch + evaluation pass)" % k,
         "value": round(upd / el, 1), "unit": "updates/s", "n_gpus": world, "steps": args.steps,
@@ -323,9 +327,17 @@ def bench_bpr(args, rank, world):
         "data": "synthetic (device-generated uniform unique pairs, seed %d)" % seed,
         "config": {"workload": "%s: BPR %d users x %d items, %d positives x %d negatives, k=%d"
                    % (args.config, nu, ni, nnz, num_neg, k)},
-        "roofline": {"kernel": "bpr_epoch_kernel", "bound": "hbm",
-                     "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 4),
+        # The epoch is bound by the chip-wide float-atomic rate (MI355X_MICROARCH.md "Global
+        # float atomics": ≈1.3 TB/s of added bytes): per positive the item rows q_p and the
+        # num_neg q_n are added atomically (the user row is a plain store); the HBM fraction of
+        # the algorithmic bytes (≈1.6 KB per update) is reported beside it
+        "roofline": {"kernel": "bpr_epoch_kernel", "bound": "l2_atomic",
+                     "achieved": round(atomic_by / sec / 1e9, 1), "peak": PEAK_ATOMIC_GBS,
+                     "unit": "GB/s", "frac": round(atomic_by / sec / 1e9 / PEAK_ATOMIC_GBS, 4),
+                     "atomic_bytes_per_launch": atomic_by,
+                     "hbm": {"achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS,
+                             "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 4),
+                             "bytes_per_launch": by},
                      "launch_ms": round(sec * 1e3, 3)},
         "eval_loss": loss,
     }
@@ -335,16 +347,23 @@ def bench_bpr(args, rank, world):
                             "traffic_source": tsrc})
     if args.cpu_baseline != "none" and rank == 0:
         # one full reference-structure Hogwild epoch (BPREngine::optimize with
-        # numHogwildThreads = nthreads) + its evaluation pass, from the device's factors
+        # numHogwildThreads = nthreads) + its evaluation pass, from the device's factors, at
+        # the learning rate the NEXT epoch uses (lr·decay^epochs, BPREngine.cpp:169-171); the
+        # device runs that same next epoch from the same state, so both eval losses are
+        # like for like (round 2 gave the port the undecayed lr: 0.05 late in training makes
+        # the item factors grow and the loss rise, 0.56 → 2.44)
         po, _ = oracle_lib()
         nthreads, host = cpu_share()
-        log("c4: CPU baseline (one Hogwild epoch, %d threads)" % nthreads)
+        e_next = args.warmup + args.steps
+        lr_next = lr * 0.9 ** e_next
+        log("c4: CPU baseline (one Hogwild epoch, %d threads, lr %.4g)" % (nthreads, lr_next))
         U, I = ctx.factors(0), ctx.factors(1)
         b = np.zeros(ni)
         users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(urp))
         perm = np.random.default_rng(seed).permutation(nnz)
         t_up, t_ev, closs = po.bpr_hogwild_epoch(U, I, b, users[perm], ucol[perm], ni, num_neg,
-                                                 nthreads, seed, lr, *lam, False, trip)
+                                                 nthreads, seed, lr_next, *lam, False, trip)
+        dloss = step(e_next)  # the device's same next epoch (untimed)
         t = t_up + t_ev
         out["cpu_baseline"] = {"value": round(nnz * num_neg / t, 1), "unit": "updates/s",
                                "cores": nthreads, "kind": "port", "ms_per_epoch": round(t * 1e3, 1),
@@ -352,7 +371,9 @@ def bench_bpr(args, rank, world):
                                          "evaluation pass of the reference-structure port on "
                                          "this workload: %.1f s + %.1f s" % (nthreads, nnz * num_neg,
                                                                              t_up, t_ev),
-                               "detail": {"host": host, "eval_loss": closs / len(trip)}}
+                               "detail": {"host": host, "lr": lr_next,
+                                          "eval_loss": closs / len(trip),
+                                          "device_eval_loss_same_epoch": dloss}}
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -205,7 +205,9 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 // chunk's (column, value) pairs are loaded a whole chunk ahead.
 template <typename T, int NT>
 constexpr int plain_depth() {
-  return (sizeof(T) == 8 && NT > 4) ? 2 : 4;  // fp64 k > 64: one wave with the whole file
+  // (fp64 k > 64 keeps its own one-step loop: gram_plain's ring spills 546 VGPRs there even
+  // with VGPR-form accumulators)
+  return (sizeof(T) == 8 && NT > 4) ? 2 : 4;
 }
 template <int J>
 __device__ __forceinline__ int row_bcast(int v) {
@@ -364,7 +366,7 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
 #define QMFX_F64_RING 7
 #endif
 #ifndef QMFX_F64_GLDS
-#define QMFX_F64_GLDS 1
+#define QMFX_F64_GLDS 0
 #endif
 template <typename T, int NT>
 constexpr bool f64_glds() {
@@ -420,31 +422,55 @@ __device__ __forceinline__ void gram_f64_glds(const SolveArgs<double>& a, int64_
   auto issue_meta = [&](int c) {
     const int e = 64 * c + lane < n ? 64 * c + lane : n - 1;
     const int64_t idx = beg + e;
-    uint32_t* m = meta + (c & 3) * 192;
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(meta + (c & 3) * 192));
     const uint32_t* v32 = reinterpret_cast<const uint32_t*>(a.val + idx);
-    __builtin_amdgcn_global_load_lds((glds_src_t)(a.col + idx), (glds_dst_t)m, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((glds_src_t)v32, (glds_dst_t)(m + 64), 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((glds_src_t)(v32 + 1), (glds_dst_t)(m + 128), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((glds_src_t)(a.col + idx), (glds_dst_t)(uintptr_t)m, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((glds_src_t)v32, (glds_dst_t)(uintptr_t)(m + 256), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((glds_src_t)(v32 + 1), (glds_dst_t)(uintptr_t)(m + 512), 4, 0,
+                                     0);
   };
-  // step u's 4 rows → ring slot u % D: wave-uniform columns from the metadata (the zero row
-  // past the end); instruction i moves bytes 1024 i .. 1024 i + 1023 of the 4-row block
-  auto issue_rows = [&](int u, int slot) {
+  // step u's 4 column indices from the metadata (asm read; the caller waits lgkmcnt)
+  auto read_cols = [&](int u) {
     const int e0 = 4 * u;
-    u32x4_t c4 = ds_read_u32x4(lds_addr(meta + ((e0 >> 6) & 3) * 192 + (e0 & 63)));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4)::"memory");
-    uint32_t cs[4] = {c4[0], c4[1], c4[2], c4[3]};
+    return ds_read_u32x4(lds_addr(meta + ((e0 >> 6) & 3) * 192 + (e0 & 63)));
+  };
+  // → wave-uniform columns (the zero row past the row's end)
+  auto uniform_cols = [&](int u, const u32x4_t& c4, uint32_t (&cs)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      cs[i] = e0 + i < n ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cs[i]) : zrow;
+      cs[i] = 4 * u + i < n ? (uint32_t)__builtin_amdgcn_readfirstlane((int)c4[i]) : zrow;
+  };
+  // step u's 4 rows → ring slot `slot`; instruction i moves bytes 1024 i .. 1024 i + 1023 of
+  // the 4-row block
+  auto issue_rows = [&](const uint32_t (&cs)[4], int slot) {
     double* dst = ring + slot * (4 * KP);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int b = 1024 * i + 16 * lane;
-      const int r = b / (KP * 8);
-      const uint32_t col = r == 0 ? cs[0] : r == 1 ? cs[1] : r == 2 ? cs[2] : cs[3];
+      uint32_t col;
+      if constexpr (KP * 8 == 1024) {
+        col = cs[i];  // k = 128: instruction i is row i
+      } else {
+        const int r = b / (KP * 8);
+        col = r == 0 ? cs[0] : r == 1 ? cs[1] : r == 2 ? cs[2] : cs[3];
+      }
       const double* src = a.Y + (uint64_t)col * KP + (b % (KP * 8)) / 8;
-      __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)(dst + 128 * i), 16, 0, 0);
+      // the LDS destination must be wave-uniform (M0): readfirstlane keeps the compiler from
+      // wrapping the load in a waterfall loop over a VGPR-held address
+      const uint32_t da = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(dst + 128 * i));
+      __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)(uintptr_t)da, 16, 0, 0);
     }
+  };
+  // step s's operands: lane (cl, kk) takes signal 4s + kk (its NT values, and the value's two
+  // words from metadata columns 64 + e and 128 + e)
+  auto read_step = [&](int s, int slot, double (&y)[NT], uint32_t& vlo, uint32_t& vhi) {
+    const uint32_t ya = lds_addr(ring + slot * (4 * KP) + kk * KP + cl);
+    [&]<int... Q>(std::integer_sequence<int, Q...>) {
+      ((y[Q] = ds_read_f64<128 * Q>(ya)), ...);
+    }(std::make_integer_sequence<int, NT>{});
+    const uint32_t ma = lds_addr(meta + ((s >> 4) & 3) * 192 + ((4 * s + kk) & 63));
+    asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(vlo) : "v"(ma));
+    asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(vhi) : "v"(ma));
   };
   // prologue: the first two chunks' metadata, then steps 0 .. D-2 (and chunk 2's metadata
   // with step 0, as the loop does for every chunk's first step)
@@ -453,39 +479,52 @@ __device__ __forceinline__ void gram_f64_glds(const SolveArgs<double>& a, int64_
   wait_vmcnt<0>();
 #pragma unroll
   for (int u = 0; u < D - 1; ++u) {
-    issue_rows(u, u);
+    u32x4_t c4 = read_cols(u);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4)::"memory");
+    uint32_t cs[4];
+    uniform_cols(u, c4, cs);
+    issue_rows(cs, u);
     if (u % 16 == 0) issue_meta(u / 16 + 2);
   }
-  int slot_use = 0, slot_issue = D - 1;
-  const int S = 16 * nch;
-  for (int s = 0; s < S; ++s) {
-    const int u = s + D - 1;
-    issue_rows(u, slot_issue);
-    if ((u & 15) == 0) issue_meta((u >> 4) + 2);
-    slot_issue = slot_issue + 1 == D ? 0 : slot_issue + 1;
-    // loads issued after step s's: NI per later step, plus a chunk's metadata when one of
-    // the steps s+1 .. s+D-1 opened a chunk (a multiple of 16 in that range)
-    if (((s + 16) & ~15) <= s + D - 1)
-      wait_vmcnt<NI * (D - 1) + NM>();
-    else
-      wait_vmcnt<NI * (D - 1)>();
-    // operands of step s: lane (cl, kk) takes signal 4s + kk
-    const uint32_t ya = lds_addr(ring + slot_use * (4 * KP) + kk * KP + cl);
-    slot_use = slot_use + 1 == D ? 0 : slot_use + 1;
-    double y[NT];
-    [&]<int... Q>(std::integer_sequence<int, Q...>) {
-      ((y[Q] = ds_read_f64<128 * Q>(ya)), ...);
-    }(std::make_integer_sequence<int, NT>{});
-    const int e = 4 * s + kk;
-    // the value's two words (metadata column 64 + e and 128 + e)
-    const uint32_t ma = lds_addr(meta + ((s >> 4) & 3) * 192 + (e & 63));
-    uint32_t vlo, vhi;
-    asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(vlo) : "v"(ma));
-    asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(vhi) : "v"(ma));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // step 0's operands and step D-1's columns
+  wait_vmcnt<NI * (D - 2)>();
+  double y[NT];
+  uint32_t vlo, vhi;
+  read_step(0, 0, y, vlo, vhi);
+  u32x4_t c4 = read_cols(D - 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4), "+v"(vlo), "+v"(vhi)::"memory");
 #pragma unroll
-    for (int q = 0; q < NT; ++q) asm volatile("" : "+v"(y[q]));
-    asm volatile("" : "+v"(vlo), "+v"(vhi));
+  for (int q = 0; q < NT; ++q) asm volatile("" : "+v"(y[q]));
+  int slot_next = 1, slot_issue = D - 1;
+  const int S = 16 * nch;
+  // Iteration s: issue step s+D-1's rows (columns read one iteration earlier), wait for step
+  // s+1's rows, read step s+1's operands and step s+D's columns, THEN run step s's MFMAs
+  // with the operands read one iteration earlier, and wait for the reads only after them:
+  // the LDS latency hides behind the MFMAs instead of stalling each step twice.
+  for (int s = 0; s < S; ++s) {
+    {
+      uint32_t cs[4];
+      uniform_cols(s + D - 1, c4, cs);
+      issue_rows(cs, slot_issue);
+    }
+    if (((s + D - 1) & 15) == 0) issue_meta(((s + D - 1) >> 4) + 2);
+    slot_issue = slot_issue + 1 == D ? 0 : slot_issue + 1;
+    // loads issued after step s+1's: NI for each of steps s+2 .. s+D-1, plus a chunk's
+    // metadata when one of those opened a chunk (a metadata load issued with step s+1 itself
+    // is waited for too: conservative)
+    if (((s + 2 + 15) & ~15) <= s + D - 1)
+      wait_vmcnt<NI * (D - 2) + NM>();
+    else
+      wait_vmcnt<NI * (D - 2)>();
+    double yn[NT];
+    uint32_t vlon, vhin;
+    read_step(s + 1, slot_next, yn, vlon, vhin);
+    slot_next = slot_next + 1 == D ? 0 : slot_next + 1;
+    c4 = read_cols(s + D);
+    // the reads stay ahead of the MFMAs (the scheduler would otherwise sink them below)
+    __builtin_amdgcn_sched_barrier(0);
+    // step s
+    const int e = 4 * s + kk;
     const double v =
         e < n ? __builtin_bit_cast(double, (unsigned long long)vlo | ((unsigned long long)vhi << 32))
               : 0.0;
@@ -506,6 +545,15 @@ __device__ __forceinline__ void gram_f64_glds(const SolveArgs<double>& a, int64_
         acc[t] = M::mma(y[I], wy[J2], acc[t]);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // (and the wait stays behind them)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4), "+v"(vlon), "+v"(vhin)::"memory");
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      asm volatile("" : "+v"(yn[q]));
+      y[q] = yn[q];
+    }
+    vlo = vlon;
+    vhi = vhin;
   }
   // the ring shares LDS with the Cholesky: every DMA (the dummy tail loads too) lands first
   wait_vmcnt<0>();
@@ -623,9 +671,12 @@ void wals_direct_kernel(SolveArgs<T> a) {
     } else if constexpr (sizeof(T) == 8 && NT > 4) {
       // fp64 k > 64 (one wave, accumulators across the whole register file): the ring of
       // gram_plain costs more spills than its deeper prefetch gains; one step ahead
+      // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
+      // so they contribute exactly nothing without per-value selects (only Σc needs the
+      // validity)
       for (int64_t base = beg; base < end; base += 64) {
         const int nst = (int)(end - base < 64 ? end - base : 64);
-        const int cr = lane < nst ? a.col[base + lane] : 0;
+        const int cr = lane < nst ? a.col[base + lane] : a.zrow;
         const T vr = lane < nst ? a.val[base + lane] : T(0);
         bool valid = kk < nst;
         T v = __shfl(vr, kk, 64);
@@ -638,15 +689,16 @@ void wals_direct_kernel(SolveArgs<T> a) {
         for (int s = 0; 4 * s < nst; ++s) {
           T yv[NT];
 #pragma unroll
-          for (int q = 0; q < NT; ++q) yv[q] = valid ? yn[q] : T(0);
-          const T w = valid ? a.alpha * v : T(0);
-          const T cw = valid ? T(1) + a.alpha * v : T(0);
+          for (int q = 0; q < NT; ++q) yv[q] = yn[q];
+          const T w = a.alpha * v;
+          const T cw = valid ? T(1) + w : T(0);
           const int jn = 4 * (s + 1) + kk;
           const bool vn = jn < nst;
           if (4 * (s + 1) < nst) {
-            const int cn = __shfl(cr, jn < 64 ? jn : 0, 64);
-            v = __shfl(vr, jn < 64 ? jn : 0, 64);
-            const T* yrow = a.Y + (uint64_t)(uint32_t)(vn ? cn : cr) * KP + cl;
+            // (lanes ≥ nst hold the zero row and v = 0)
+            const int cn = __shfl(cr, jn < 64 ? jn : 63, 64);
+            v = __shfl(vr, jn < 64 ? jn : 63, 64);
+            const T* yrow = a.Y + (uint64_t)(uint32_t)cn * KP + cl;
 #pragma unroll
             for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
           }

@@ -35,6 +35,9 @@
 #ifndef QMFX_BIG_SIG64
 #define QMFX_BIG_SIG64 16
 #endif
+#ifndef QMFX_BIG_PANEL_ALL
+#define QMFX_BIG_PANEL_ALL 1  // every wave factors the panel's diagonal block with its own rows
+#endif
 #ifndef QMFX_BIG_SPLIT
 #define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
 #endif
@@ -111,6 +114,7 @@ struct BigShared {
   T borig[C::KP];
   T xs[C::KP];
   T invd[C::KP];
+  T yd[C::KP];  // forward-solve y of each diagonal block (read by the backward solve)
   T part[C::NW * 16];
   double red[C::NW];
   int bad;  // wave 0's pivot flag, for every wave's output stores
@@ -174,6 +178,7 @@ __device__ void big_panel_head(BigShared<T, NT>& S, int p, int lane, int& bad) {
   if (lane < 16) {
     S.invd[16 * p + lane] = invv;
     S.bw[16 * p + lane] = yv;
+    S.yd[16 * p + lane] = yv;
   }
   if (live) {
 #pragma unroll
@@ -185,6 +190,64 @@ __device__ void big_panel_head(BigShared<T, NT>& S, int p, int lane, int& bad) {
   for (int idx = lane; idx < 256; idx += 64) {
     const int r = idx >> 4, c = idx & 15;
     S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
+  }
+}
+
+// Panel p on every wave at once: lanes 0..15 of each wave hold the diagonal block (factored
+// redundantly, as in the head), lanes 16..63 rows 48W + 16 .. 48W + 63 of the panel; each
+// wave runs the head's column loop on its own rows, so the serial head and the slot phase
+// behind it (and one barrier) become one step.  Wave 0 writes the diagonal block.
+template <typename T, int NT>
+__device__ void big_panel_all(BigShared<T, NT>& S, int p, int wv, int lane, int& bad) {
+  constexpr int KP = 16 * NT;
+  constexpr int PLD = BigCfg<T, NT>::PLD;
+  const int R = KP - 16 * p;
+  static_assert(48 * BigCfg<T, NT>::NW + 16 >= KP, "panel rows beyond the waves' lanes");
+  if (wv > 0 && 48 * wv + 16 >= R) return;  // no rows below the diagonal block for this wave
+  const int q = lane < 16 ? lane : 48 * wv + lane;
+  const bool live = q < R;
+  T pa[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
+  T pb = live ? S.bw[16 * p + q] : T(0);
+  T invv = T(0), yv = T(0);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    T am[16];
+#pragma unroll
+    for (int m = 1; m < 16; ++m)
+      if (m > c) am[m] = readlane(pa[c], m);
+    const T d = readlane(pa[c], c);
+    const T bc = readlane(pb, c);
+    T ljj, inv;
+    pivot_sqrt(d, ljj, inv);
+    (void)ljj;
+    bad |= !(d > T(0));
+    const bool me = lane == c;
+    invv = me ? inv : invv;
+    yv = me ? bc * inv : yv;
+    const T lq = pa[c] * inv;
+    const T lqs = lq * inv;
+    pa[c] = lq;
+    pb -= lqs * bc;
+#pragma unroll
+    for (int m = 1; m < 16; ++m)
+      if (m > c) pa[m] -= lqs * am[m];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // every wave read the diagonal block before wave 0 overwrites it: the caller's barrier
+  // after the panel orders the stores of other waves; rows ≥ 16 are disjoint per wave
+  if (lane >= 16 && live) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
+    S.bw[16 * p + q] = pb;
+  }
+  if (wv == 0 && lane < 16) {
+    // y of the diagonal block goes to S.yd: other waves may still be reading S.bw[16p..]
+    S.invd[16 * p + lane] = invv;
+    S.yd[16 * p + lane] = yv;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) S.Ldiag[(p * 16 + lane) * PLD + c] = c <= lane ? pa[c] : T(0);
   }
 }
 
@@ -551,12 +614,16 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     }
     __syncthreads();
     if (!(a.ablate & 2)) {
+#if QMFX_BIG_PANEL_ALL
+      big_panel_all<T, NT>(S, p, wv, lane, bad);
+#else
       if (wv == 0) big_panel_head<T, NT>(S, p, lane, bad);
       if (KP - 16 * p > 64) {
         __syncthreads();
         for (int base = 64 * (1 + wv); base < KP - 16 * p; base += 64 * NW)
           big_panel_slot<T, NT>(S, p, base, lane);
       }
+#endif
     }
     __syncthreads();
 #pragma unroll
@@ -604,7 +671,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     if (kk == 0) S.part[wv * 16 + cl] = part;
     __syncthreads();
     if (wv == 0) {
-      T vm = S.bw[16 * I + cl];
+      T vm = S.yd[16 * I + cl];
 #pragma unroll
       for (int w = 0; w < NW; ++w) vm -= S.part[w * 16 + cl];
       // row cl scaled by its own 1/L[cl][cl] (x_c is then row c's value itself): each step

@@ -236,7 +236,10 @@ def test_row_system_matches_oracle():
     (256, 32, 160000, "1"), (256, 32, 30000, "1"),
     # fp32 k = 256 / 128, ~100 signals per user: the n = 65..128 buckets (two signals per
     # lane)
-    (256, 32, 400000, "0"), (128, 32, 400000, "0")])
+    (256, 32, 400000, "0"), (128, 32, 400000, "0"),
+    # fp64 k = 128, ~100 signals per user: the streamed fp64 kernel's n = 65..80 bucket (two
+    # signals per lane, second ballot words, 5-tile fp64 Cholesky)
+    (128, 64, 400000, "0")])
 def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
@@ -247,8 +250,13 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatc
     u, i, v = synth(4000, 900, nnz, seed=11)  # ~7.5 (or ~40) signals per user
     v[::7] = 0.0  # zero-valued signals (Q set: c = 1, w = 0)
     o, c = make_pair(u, i, v, k, precision, seed=2)
+    if nnz == 400000:
+        # the two-signals-per-lane buckets (n > 64 → 5 or more 16-row tiles) hold rows
+        wb = c.row_classes(0)["whitened"]
+        assert wb[4] > 0, wb
     monkeypatch.setenv("QMFX_NO_WHITEN", "1")
     _, cd = make_pair(u, i, v, k, precision, seed=2)
+    assert sum(cd.row_classes(0)["whitened"]) == 0
     monkeypatch.delenv("QMFX_NO_WHITEN")
     tol = 1e-4 if precision == 32 else 1e-9
     for side in (0, 1):

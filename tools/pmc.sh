@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over one bench epoch of CFG at PREC (each counter group in its own rocprofv3
 # run, kernel-trace only) plus a --stats kernel-trace run.  Outputs under
-# gpurun_out/pmc_<CFG>_<PREC>/.  usage: CFG=c3 PREC=32 tools/r02_pmc.sh
+# gpurun_out/pmc_<CFG>_<PREC>/.  usage: CFG=c3 PREC=32 tools/pmc.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -37,7 +37,7 @@ def main(src, out):
             if c.startswith("SQ_") or c.startswith("GRBM"):
                 e[c] = v
         res[k] = e
-    json.dump({"source": "rocprofv3 --pmc, one counter group per pass (tools/r01_pmc.sh)",
+    json.dump({"source": "rocprofv3 --pmc, one counter group per pass (tools/pmc.sh)",
                "units": "bytes per dispatch; fetch doubled per the gfx950 FETCH_SIZE note",
                "kernels": res}, open(out, "w"), indent=1)
 
