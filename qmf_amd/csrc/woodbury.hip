@@ -310,6 +310,21 @@ template <int NTN>
 constexpr int wb_st_waves() {
   return NTN <= 4 ? QMFX_WB_ST_WAVES : (NTN == 5 ? 2 : 1);
 }
+// chunks in flight ahead of the one being consumed, K pass and x' pass (n ≤ 64 buckets)
+#ifndef QMFX_WBS_KD
+#define QMFX_WBS_KD 1
+#endif
+#ifndef QMFX_WBS_XD
+#define QMFX_WBS_XD 1
+#endif
+template <int NTN>
+constexpr int wbs_kdepth() {
+  return NTN <= 4 ? QMFX_WBS_KD : 1;
+}
+template <int NTN>
+constexpr int wbs_xdepth() {
+  return NTN <= 4 ? QMFX_WBS_XD : 1;
+}
 template <int NTK, int NTN>
 __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kernel(SolveArgs<float> a) {
   using M = Mfma<float>;
@@ -378,11 +393,15 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 #pragma unroll
   for (int I = 0; I < NTN; ++I) sq[I] = 0.f;
   {
-    f32x4 cur[NTN][2], nxt[NTN][2];
-    load_chunk(0, cur);
+    // a ring of KD + 1 chunk buffers: chunk s + KD is in flight while chunk s is consumed
+    constexpr int KD = wbs_kdepth<NTN>();
+    f32x4 buf[KD + 1][NTN][2];
+#pragma unroll
+    for (int s = 0; s < KD && s < NS; ++s) load_chunk(s, buf[s]);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      if (s + KD < NS) load_chunk(s + KD, buf[(s + KD) % (KD + 1)]);
+      f32x4 (&cur)[NTN][2] = buf[s % (KD + 1)];
 #if QMFX_WBS_SPLIT
       Split3 sp[NTN];
 #pragma unroll
@@ -441,14 +460,7 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
         }
       }
 #endif
-      if (s + 1 < NS) {
-#pragma unroll
-        for (int I = 0; I < NTN; ++I) {
-          cur[I][0] = nxt[I][0];
-          cur[I][1] = nxt[I][1];
-        }
-      }
-      // one chunk's splits and the next chunk's loads live at a time
+      // one chunk's splits and the next chunks' loads live at a time
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -542,12 +554,16 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 
   // x' = Zₛᵀu (and for rows with Q signals xᵀb = x'ᵀ(Zₛᵀc)), the rows gathered again
   {
-    f32x4 cur[NTN][2], nxt[NTN][2];
-    load_chunk(0, cur);
+    // XD chunks in flight (the accumulators are dead after the solve)
+    constexpr int XD = wbs_xdepth<NTN>();
+    f32x4 buf[XD + 1][NTN][2];
+#pragma unroll
+    for (int s = 0; s < XD && s < NS; ++s) load_chunk(s, buf[s]);
     double xbq = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      if (s + XD < NS) load_chunk(s + XD, buf[(s + XD) % (XD + 1)]);
+      f32x4 (&cur)[NTN][2] = buf[s % (XD + 1)];
       float sx[2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -585,13 +601,6 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
         if (bad) o = f32x4{0.f, 0.f, 0.f, 0.f};
         reinterpret_cast<f32x4*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
       }
-      if (s + 1 < NS) {
-#pragma unroll
-        for (int I = 0; I < NTN; ++I) {
-          cur[I][0] = nxt[I][0];
-          cur[I][1] = nxt[I][1];
-        }
-      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
@@ -615,7 +624,23 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 // whose register-resident Zₛ (half a row of doubles per lane) spilled.
 // ---------------------------------------------------------------------------------------
 typedef double f64x2 __attribute__((ext_vector_type(2)));
-template <int NTK, int NTN>
+// chunks in flight ahead of the one being consumed: K pass (beside the NTT accumulator
+// tiles) and x' pass (after the solve, when the accumulators are dead)
+#ifndef QMFX_WB64_KD
+#define QMFX_WB64_KD 1
+#endif
+#ifndef QMFX_WB64_XD
+#define QMFX_WB64_XD 1
+#endif
+template <int NTN>
+constexpr int wb64_kdepth() {
+  return NTN <= 4 ? QMFX_WB64_KD : 1;
+}
+template <int NTN>
+constexpr int wb64_xdepth() {
+  return NTN <= 4 ? QMFX_WB64_XD : 1;
+}
+template <int NTK, int NTN, bool TRACE = false>
 __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
   using M = Mfma<double>;
   using acc_t = typename M::acc_t;
@@ -629,6 +654,8 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
   const int lane = threadIdx.x;
   const int cl = lane & 15;
   const int kk = lane >> 4;
+  uint64_t tr[5] = {0, 0, 0, 0, 0};
+  if (TRACE) tr[0] = __builtin_amdgcn_s_memtime();
   const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
   const int64_t row = dn.row;
   const int n = dn.n;  // ≤ 16·NTN by bucketing
@@ -654,6 +681,10 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
   }
   auto bit = [](const uint64_t (&m)[H], int e) -> bool { return (m[e >> 6] >> (e & 63)) & 1; };
 
+  if (TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[1] = __builtin_amdgcn_s_memtime();
+  }
   // this lane's signals 16I + cl (padding signals read the all-zero row a.zrow)
   const f64x2* zp[NTN];
 #pragma unroll
@@ -677,11 +708,16 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
 #pragma unroll
   for (int I = 0; I < NTN; ++I) sq[I] = 0.0;
   {
-    double cur[NTN][4], nxt[NTN][4];
-    load_chunk(0, cur);
+    // a ring of KD + 1 chunk buffers: chunk s + KD is in flight while chunk s is consumed
+    // (the loop unrolls fully, so every ring index is a compile-time constant)
+    constexpr int KD = wb64_kdepth<NTN>();
+    double buf[KD + 1][NTN][4];
+#pragma unroll
+    for (int s = 0; s < KD && s < NS; ++s) load_chunk(s, buf[s]);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      if (s + KD < NS) load_chunk(s + KD, buf[(s + KD) % (KD + 1)]);
+      double (&cur)[NTN][4] = buf[s % (KD + 1)];
       if (hasQ) {
         double g[4];
 #pragma unroll
@@ -709,13 +745,7 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
           }
         }
       }
-      if (s + 1 < NS) {
-#pragma unroll
-        for (int I = 0; I < NTN; ++I)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) cur[I][c] = nxt[I][c];
-      }
-      // one chunk and the next chunk's loads live at a time
+      // one chunk and the next chunks' loads live at a time
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -740,7 +770,9 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     for (int h = 0; h < H; ++h)
       if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
+    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
     chol_solve<double, NTN>(acc, S, lane, bad);
+    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
     double xbl = 0.0;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -796,7 +828,9 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     for (int h = 0; h < H; ++h)
       if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
+    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
     chol_solve<double, NTN>(acc, S, lane, bad);
+    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       const int e = 16 * I + cl;
@@ -809,12 +843,18 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
 
   // x' = Zₛᵀu (and for rows with Q signals xᵀb = x'ᵀ(Zₛᵀc)), the rows gathered again
   {
-    double cur[NTN][4], nxt[NTN][4];
-    load_chunk(0, cur);
+    // XD chunks in flight: the Gram's accumulators are dead here, so the x' pass can hold
+    // a deeper ring than the K pass (each chunk costs little compute: its loads would
+    // otherwise be waited for one after the other)
+    constexpr int XD = wb64_xdepth<NTN>();
+    double buf[XD + 1][NTN][4];
+#pragma unroll
+    for (int s = 0; s < XD && s < NS; ++s) load_chunk(s, buf[s]);
     double xbq = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) load_chunk(s + 1, nxt);
+      if (s + XD < NS) load_chunk(s + XD, buf[(s + XD) % (XD + 1)]);
+      double (&cur)[NTN][4] = buf[s % (XD + 1)];
       double sx[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -843,12 +883,6 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
         if (bad) o = f64x2{0.0, 0.0};
         reinterpret_cast<f64x2*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
       }
-      if (s + 1 < NS) {
-#pragma unroll
-        for (int I = 0; I < NTN; ++I)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) cur[I][c] = nxt[I][c];
-      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
@@ -860,6 +894,18 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
   if (lane == 0) {
     a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
     if (bad && a.status) a.status[row] = 1;
+  }
+  if (TRACE && lane == 0) {
+    tr[4] = __builtin_amdgcn_s_memtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* o = a.trace + 8 * (a.row_begin + blockIdx.x);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) o[j] = tr[j];
+    o[5] = hw | ((uint64_t)xcc << 32);
+    o[6] = (uint64_t)n;
+    o[7] = (uint64_t)row;
   }
 }
 
@@ -1391,8 +1437,12 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
   if (!a.desc) return hipErrorInvalidValue;
 #define QMFX_WBS64(N)                                                                      \
   return launch_row_chunks(a, 64, [&](const SolveArgs<double>& c) {                        \
-    hipLaunchKernelGGL((wals_woodbury_st64_kernel<NTK, N>), dim3((unsigned)c.nrows), dim3(64), \
-                       0, s, c);                                                           \
+    if (c.trace)                                                                           \
+      hipLaunchKernelGGL((wals_woodbury_st64_kernel<NTK, N, true>), dim3((unsigned)c.nrows), \
+                         dim3(64), 0, s, c);                                               \
+    else                                                                                   \
+      hipLaunchKernelGGL((wals_woodbury_st64_kernel<NTK, N>), dim3((unsigned)c.nrows),     \
+                         dim3(64), 0, s, c);                                               \
   })
   switch (ntn) {
     case 1: QMFX_WBS64(1);
