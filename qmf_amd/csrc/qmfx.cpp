@@ -1055,7 +1055,7 @@ int half_piece(qmfx_ctx* c, int j) {
         SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)c->Z,
                             nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
                             pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
-                            nullptr, nullptr, (int32_t)c->z_cap};
+                            nullptr, trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
         HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->ksel, c->stream));
       }
     }
