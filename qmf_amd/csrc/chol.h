@@ -23,10 +23,6 @@ namespace qmfx {
 #ifndef QMFX_CHOL_PK
 #define QMFX_CHOL_PK 1
 #endif
-// fp64 panels without a square root in the column loop (QMFX_CHOL_FF, see chol_solve)
-#ifndef QMFX_CHOL_FF
-#define QMFX_CHOL_FF 0
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T>
@@ -95,7 +91,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
   constexpr int PLD = CholShared<T, NT>::PLD;
   const int cl = lane & 15;
   const int kk = lane >> 4;
-  constexpr bool FF = sizeof(T) == 8 && QMFX_CHOL_FF;
 #pragma unroll
   for (int p = 0; p < NT; ++p) {
     const int R = KP - 16 * p;
@@ -118,71 +113,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     }
     // lanes 0..15 collect the panel's 1/L[c][c] and y_c (lane c), stored once per panel
     T invv = T(0), yv = T(0);
-    if constexpr (FF) {
-      // Square-root-free panel (fp64): column c replaces the trailing part of the panel by
-      // σ_c·(d_c·Ã − ã_c ã_cᵀ), with σ_c = 2^-e the exact power of two that brings σ_c·d_c
-      // into [½, 1) (Ã = the Schur complement divided by t_c: t_0 = 1, t_{c+1} =
-      // t_c/(σ_c d_c), so Ã stays in range).  The column loop's critical path is then
-      // readlane → frexp/ldexp → FMA → readlane, with no rsq and Newton steps per column.
-      // With u_c = 1/t_c (one multiply per column, off that path), the true factor is
-      // L[q][c] = Ã[q][c]·f_c with f_c = 1/√(u_c d_c), 1/L[c][c] = u_c·f_c and y_c = b̃_c·f_c:
-      // one vector rsq for the panel's 16 columns after the loop.  A pivot ≤ 0 (or NaN)
-      // makes f_c NaN or ∞, which the (0, ∞) test below flags.
-      T u = T(1), ucl = T(0), ucn = T(0), yraw = T(0);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        T am[16];
-#pragma unroll
-        for (int m = 1; m < 16; ++m)
-          if (m > c) am[m] = readlane(pa[0][c], m);
-        const T d = readlane(pa[0][c], c);
-        const T bc = readlane(pb[0], c);
-        const int e = __builtin_amdgcn_frexp_exp(d);
-        const T ds = __builtin_ldexp(d, -e);  // σ_c·d_c
-        const bool me = lane == c;
-        ucl = me ? u : ucl;
-        ucn = me ? u * d : ucn;
-        yraw = me ? bc : yraw;
-        u *= ds;
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          if (64 * s < R) {
-            const T a = __builtin_ldexp(pa[s][c], -e);  // σ_c·ã_q
-            pb[s] = __builtin_fma(ds, pb[s], -(a * bc));
-#pragma unroll
-            for (int m = 1; m < 16; ++m)
-              if (m > c) pa[s][m] = __builtin_fma(ds, pa[s][m], -(a * am[m]));
-          }
-        }
-#pragma unroll
-        for (int s = 1; s < SLOTS; ++s) {
-          if (64 * s < R) {
-#pragma unroll
-            for (int m = 0; m < 16; ++m)
-              if (m > c) asm volatile("" : "+v"(pa[s][m]));
-            asm volatile("" : "+v"(pb[s]));
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      T lf, f;
-      pivot_sqrt(ucn, lf, f);  // lane c: f_c = 1/√(u_c d_c)
-      (void)lf;
-      invv = ucl * f;
-      yv = yraw * f;
-      T fc[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) fc[c] = readlane(f, c);
-      const T bsc = T(1) / u;  // t_16: the trailing rows' b̃ back to b
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        if (64 * s < R) {
-#pragma unroll
-          for (int c = 0; c < 16; ++c) pa[s][c] *= fc[c];
-          pb[s] *= bsc;
-        }
-      }
-    } else {
+    {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the

@@ -296,12 +296,14 @@ bool use_big_rows(const qmfx_ctx* c) {
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
   // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) and fp64
-  // k = 80..128 (NT = 5..8, the multi-wave whitened kernel)
+  // k = 80..128 and 256 (NT = 5..8 and 16: the streamed fp64 kernel)
   if (use_big(c)) {
     // fp32 k = 256: the streamed kernel takes n ≤ 128 (two signals per lane past 64), the
     // multi-wave one (QMFX_WB_MW=1) n ≤ 64
     if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256(c->ksel) : 0;
     if (c->nt == 8) return whitened_max_ntn_f64_k128(c->ksel);
+    // fp64 k = 256: the streamed fp64 kernel (n ≤ 80), or every row on the big kernel
+    if (c->nt == 16) return c->ksel.wb_st64 ? whitened_max_ntn_f64_k128(c->ksel) : 0;
     return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
   }
   int m = c->nt / 2;

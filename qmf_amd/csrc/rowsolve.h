@@ -27,10 +27,7 @@ __device__ __forceinline__ void pivot_sqrt(float d, float& l, float& inv) {
 #define QMFX_F64_RSQ_NR 1
 #endif
 __device__ __forceinline__ void pivot_sqrt(double d, double& l, double& inv) {
-#if QMFX_F64_RSQ_NR == 2  // timing experiment only (≈1e-7 relative pivots): no Newton steps
-  inv = __builtin_amdgcn_rsq(d);
-  l = d * inv;
-#elif QMFX_F64_RSQ_NR
+#if QMFX_F64_RSQ_NR
   const double y = __builtin_amdgcn_rsq(d);
   double g = d * y, h = 0.5 * y;
   double r = __builtin_fma(-g, h, 0.5);

@@ -616,7 +616,7 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 }
 
 // ---------------------------------------------------------------------------------------
-// Whitened row kernel, streamed, fp64 (k = 80..128): the fp32 streamed kernel's plan on the
+// Whitened row kernel, streamed, fp64 (k = 80..128 and 256): the fp32 streamed kernel's plan on the
 // fp64 matrix path.  K = Zₛ Zₛᵀ accumulates over 16-column chunks of the gathered rows with
 // the next chunk in flight: lane (i, g) holds columns 16s + 4g .. +3 of signal 16I + i, and
 // its j-th value is the K index of 16x16x4 f64 MFMA j (exact fp64 products, no split).
@@ -1453,9 +1453,9 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
     case 4:
       if constexpr (NTK >= 8) QMFX_WBS64(4);
       return hipErrorInvalidValue;
-    // n = 65..80 (two signals per lane) at k = 128 (n > 80 spills: direct)
+    // n = 65..80 (two signals per lane) at k = 128 and 256 (n > 80 spills: direct)
     case 5:
-      if constexpr (NTK == 8) QMFX_WBS64(5);
+      if constexpr (NTK == 8 || NTK == 16) QMFX_WBS64(5);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -1562,14 +1562,15 @@ hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, cons
 }
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn,
                                 const KernelSel& ks, hipStream_t s) {
-  // one wave up to k = 64; k = 80..128 on the streamed kernel (QMFX_WB_ST64=0: the
-  // multi-wave one)
-  if (nt >= 5 && nt <= 8 && ks.wb_st64) {
+  // one wave up to k = 64; k = 80..128 and 256 on the streamed kernel (QMFX_WB_ST64=0: the
+  // multi-wave one up to k = 128, the big kernel at k = 256)
+  if (((nt >= 5 && nt <= 8) || nt == 16) && ks.wb_st64) {
     switch (nt) {
       case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
       case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
       case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);
       case 8: return launch_woodbury_st64_ntk<8>(a, ntn, s);
+      case 16: return launch_woodbury_st64_ntk<16>(a, ntn, s);
       default: break;
     }
   }
@@ -1595,7 +1596,7 @@ hipError_t launch_whiten(const double* in, double* out, const int64_t* order, in
                          int nt, const double* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s) {
 #define CALL(N) launch_whiten_nt<double, N>(in, out, order, nrows, Linv, rowloss, lambda, unwhiten, s)
-  QMFX_NT_SWITCH(nt, CALL)
+  QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* Linv,
@@ -1607,7 +1608,7 @@ hipError_t launch_chol_inv(const float* G, int nt, int k, double lambda, float* 
 hipError_t launch_chol_inv(const double* G, int nt, int k, double lambda, double* Linv,
                            int32_t* status, double* scratch, hipStream_t s) {
 #define CALL(N) launch_chol_inv_nt<double, N>(G, k, lambda, Linv, status, scratch, s)
-  QMFX_NT_SWITCH(nt, CALL)
+  QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
 #endif  // QMFX_KERNELS_ONLY

@@ -239,7 +239,10 @@ def test_row_system_matches_oracle():
     (256, 32, 400000, "0"), (128, 32, 400000, "0"),
     # fp64 k = 128, ~100 signals per user: the streamed fp64 kernel's n = 65..80 bucket (two
     # signals per lane, second ballot words, 5-tile fp64 Cholesky)
-    (128, 64, 400000, "0")])
+    (128, 64, 400000, "0"),
+    # fp64 k = 256 (C5 at the reference's precision): the streamed fp64 kernel beside the
+    # big k×k kernel, every bucket up to n = 80
+    (256, 64, 30000, "0"), (256, 64, 160000, "0"), (256, 64, 400000, "0")])
 def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
