@@ -743,19 +743,29 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void gram_tiles_kernel(
     acc[s] = acc_t{0, 0, 0, 0};
   }
 
+  // the next stage's rows are loaded into registers while this stage's MFMAs run (the
+  // same rows in the same order: the partials are bit-identical to a load-then-compute loop)
+  vec_t nx[TRIPS];
+  auto fetch = [&](int64_t e0) {
+#pragma unroll
+    for (int t = 0; t < TRIPS; ++t) {
+      const int ch = tid + C::NTHR * t;
+      const int64_t e = e0 + ch / CPR;
+      nx[t] = (ch < SIG * CPR && e < r1)
+                  ? *(reinterpret_cast<const vec_t*>(Y + e * KP) + ch % CPR)
+                  : vec_t{};
+    }
+  };
+  if (r0 < r1) fetch(r0);
   for (int64_t e0 = r0; e0 < r1; e0 += SIG) {
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < TRIPS; ++t) {
       const int ch = tid + C::NTHR * t;
-      if (ch < SIG * CPR) {
-        const int64_t e = e0 + ch / CPR;
-        const vec_t v = e < r1 ? *(reinterpret_cast<const vec_t*>(Y + e * KP) + ch % CPR)
-                               : vec_t{};
-        reinterpret_cast<vec_t*>(stage)[ch] = v;
-      }
+      if (ch < SIG * CPR) reinterpret_cast<vec_t*>(stage)[ch] = nx[t];
     }
     __syncthreads();
+    if (e0 + SIG < r1) fetch(e0 + SIG);
     if constexpr (C::REUSE) {
       auto step = [&](auto wtag) {
 #pragma unroll 2
