@@ -536,6 +536,9 @@ def main():
     traffic, tsrc = pmc_traffic(args.config, args.precision, dom, k)
     roof.update({"traffic": round(traffic, 0) if traffic else None,
                  "traffic_algorithmic_ratio": round(traffic / d["bytes_per_launch"], 3) if traffic else None,
+                 # the counted L2↔fabric bytes per launch over this run's launch time (MALL hits
+                 # included: the fabric rate the class runs at)
+                 "traffic_gbs": round(traffic / (d["launch_ms"] / 1e3) / 1e9, 1) if traffic else None,
                  "traffic_source": tsrc, "launch_ms": d["launch_ms"], "classes": classes})
     half = ctx.kernel_stats(2)
     epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
