@@ -1183,9 +1183,15 @@ __global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs
 //   whiten:   Z[r] = Linv · Y[r]     (z = L⁻¹ y)            rows 0..n-1, 16 per wave
 //   unwhiten: X[r] = Linvᵀ · X'[r]   (x = L⁻ᵀ x') in place, rows from `order`; also
 //             rowloss[r] −= λ‖x‖².
-// One wave computes a 16-row × KP block with NT accumulator tiles; the zero upper
+// One wave computes QMFX_WHITEN_RG 16-row × KP blocks with NT accumulator tiles each (two: each
+// L⁻¹ fragment serves two MFMAs; C3 fp64 382.9 → 381.5 ms/epoch); the zero upper
 // triangle of Linv is skipped.
 // ---------------------------------------------------------------------------------------
+// row groups of 16 per wave in the whitening GEMMs: each L⁻¹ operand fragment is loaded once
+// and used for RG groups' MFMAs
+#ifndef QMFX_WHITEN_RG
+#define QMFX_WHITEN_RG 2
+#endif
 template <typename T, int NT, bool UNWHITEN>
 __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const int64_t* order,
                                                      int64_t nrows, const T* __restrict__ Linv,
@@ -1193,52 +1199,74 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   constexpr int KP = 16 * NT;
+  constexpr int RG = QMFX_WHITEN_RG;
   const int lane = threadIdx.x & 63;
   const int cl = lane & 15;
   const int kk = lane >> 4;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-  if (r0 >= nrows) return;
-  const int64_t ra = r0 + cl < nrows ? r0 + cl : nrows - 1;
-  const int64_t rowa = UNWHITEN ? order[ra] : ra;
-  acc_t acc[NT];
+  const int64_t rw = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (16 * RG);
+  if (rw >= nrows) return;
+  int64_t rowa[RG];
 #pragma unroll
-  for (int J = 0; J < NT; ++J) acc[J] = acc_t{0, 0, 0, 0};
+  for (int g = 0; g < RG; ++g) {
+    const int64_t r = rw + 16 * g + cl;
+    const int64_t ra = r < nrows ? r : nrows - 1;
+    rowa[g] = UNWHITEN ? order[ra] : ra;
+  }
+  acc_t acc[RG][NT];
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+#pragma unroll
+    for (int J = 0; J < NT; ++J) acc[g][J] = acc_t{0, 0, 0, 0};
 #pragma unroll
   for (int s = 0; s < KP / 4; ++s) {
     const int m = 4 * s + kk;
-    const T av = in[rowa * KP + m];
+    T av[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) av[g] = in[rowa[g] * KP + m];
 #pragma unroll
     for (int J = 0; J < NT; ++J) {
       const int j = 16 * J + cl;
       if (UNWHITEN) {
         // x_j = Σ_m x'_m Linv[m][j]: nonzero only for m ≥ j
-        if (4 * s + 3 >= 16 * J) acc[J] = M::mma(av, Linv[m * KP + j], acc[J]);
+        if (4 * s + 3 >= 16 * J) {
+          const T bv = Linv[m * KP + j];
+#pragma unroll
+          for (int g = 0; g < RG; ++g) acc[g][J] = M::mma(av[g], bv, acc[g][J]);
+        }
       } else {
         // z_j = Σ_m Linv[j][m] y_m: nonzero only for m ≤ j
-        if (4 * s <= 16 * J + 15) acc[J] = M::mma(av, Linv[j * KP + m], acc[J]);
+        if (4 * s <= 16 * J + 15) {
+          const T bv = Linv[j * KP + m];
+#pragma unroll
+          for (int g = 0; g < RG; ++g) acc[g][J] = M::mma(av[g], bv, acc[g][J]);
+        }
       }
     }
   }
   // all reads of this wave's rows are done before any write (in-place unwhitening)
-  T ss[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t ro = r0 + M::crow(lane, r);
-    if (ro < nrows) {
-      const int64_t rowo = UNWHITEN ? order[ro] : ro;
-#pragma unroll
-      for (int J = 0; J < NT; ++J) {
-        out[rowo * KP + 16 * J + cl] = acc[J][r];
-        ss[r] += acc[J][r] * acc[J][r];
-      }
-    }
-  }
-  if (UNWHITEN) {
+  for (int g = 0; g < RG; ++g) {
+    const int64_t r0 = rw + 16 * g;
+    T ss[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const T tot = row16_sum(ss[r]);
       const int64_t ro = r0 + M::crow(lane, r);
-      if (cl == 0 && ro < nrows) rowloss[order[ro]] -= lambda * (double)tot;
+      if (ro < nrows) {
+        const int64_t rowo = UNWHITEN ? order[ro] : ro;
+#pragma unroll
+        for (int J = 0; J < NT; ++J) {
+          out[rowo * KP + 16 * J + cl] = acc[g][J][r];
+          ss[r] += acc[g][J][r] * acc[g][J][r];
+        }
+      }
+    }
+    if (UNWHITEN) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const T tot = row16_sum(ss[r]);
+        const int64_t ro = r0 + M::crow(lane, r);
+        if (cl == 0 && ro < nrows) rowloss[order[ro]] -= lambda * (double)tot;
+      }
     }
   }
 }
@@ -1473,7 +1501,7 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
                                    const T* Linv, double* rowloss, double lambda, bool unwhiten,
                                    hipStream_t s) {
   if (nrows <= 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((nrows + 63) / 64);
+  const unsigned blocks = (unsigned)((nrows + 64 * QMFX_WHITEN_RG - 1) / (64 * QMFX_WHITEN_RG));
   if (unwhiten)
     hipLaunchKernelGGL((whiten_kernel<T, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, order,
                        nrows, Linv, rowloss, lambda);
