@@ -140,10 +140,9 @@ def cpu_baseline(ctx, cfg, nthreads, budget_s=20.0):
         remap = np.searchsorted(uniq, cols).astype(np.int32)
         srp = np.concatenate([[0], np.cumsum([s.size for s in seg])]).astype(np.int64)
         dummy_rp = np.zeros(len(uniq) + 1, np.int64)
-        args = (srp, remap, val[idx].astype(np.float32), dummy_rp,
-                np.zeros(1, np.int32), np.zeros(1, np.float32)) if side == 0 else \
-               (dummy_rp, np.zeros(1, np.int32), np.zeros(1, np.float32), srp, remap,
-                val[idx].astype(np.float32))
+        args = (srp, remap, val[idx], dummy_rp,
+                np.zeros(1, np.int32), np.zeros(1)) if side == 0 else \
+               (dummy_rp, np.zeros(1, np.int32), np.zeros(1), srp, remap, val[idx])
         nsu, nsi = (S, len(uniq)) if side == 0 else (len(uniq), S)
         o = po.OracleWALS.from_csr(nsu, nsi, *args, k, LAM, ALPHA)
         o.set_factors(1 - side, Y[uniq])
@@ -190,7 +189,7 @@ def cpu_epoch(ctx, cfg, nthreads):
                "t_build": round(t_build, 3), "loss": loss}
 
 
-def parity_check(ctx, cfg, nthreads, nsample=1000):
+def parity_check(ctx, cfg, nthreads, cfg_precision, nsample=1000):
     """Full-size parity: one more (untimed) epoch; `nsample` rows of each half are re-solved
     by the oracle's updateFactorsForOne (WALSEngine.cpp:266-310) against the fixed side the
     device used (its own values), and compared with the device's rows and row losses."""
@@ -218,9 +217,12 @@ def parity_check(ctx, cfg, nthreads, nsample=1000):
                                 "oracle_s": round(time.perf_counter() - t0, 2)}
         worst = max(worst, float(row_err.max()))
         del rp, col, val
+    # the bar of the precision measured: fp64 is held to the GPU tests' 1e-9 (an fp64
+    # regression between 1e-9 and 1e-4 must not print pass), fp32 to north_star's 1e-4
+    tol = 1e-9 if cfg_precision == 64 else 1e-4
     out["max_rel_err"] = worst
-    out["tolerance"] = 1e-4
-    out["pass"] = bool(worst <= 1e-4)
+    out["tolerance"] = tol
+    out["pass"] = bool(worst <= tol)
     return out
 
 
@@ -250,7 +252,8 @@ def pmc_traffic(config, precision, cls, k):
     tot, hit = 0.0, False
     for name, e in ks.items():
         if any(name.startswith(p) for p in pats) and "fetch_bytes" in e and "write_bytes" in e:
-            tot += e["fetch_bytes"] + e["write_bytes"]
+            # the largest dispatch = the class's large launch (older summaries: the mean)
+            tot += e.get("fetch_bytes_max", e["fetch_bytes"]) + e.get("write_bytes_max", e["write_bytes"])
             hit = True
     return (tot if hit else None), os.path.relpath(files[-1], ROOT)
 
@@ -376,6 +379,43 @@ def bench_bpr(args, rank, world):
                                           "device_eval_loss_same_epoch": dloss}}
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def roofline_classes(ctx, k, precision):
+    """Per kernel class: its LARGE launch (the side whose launches take longest: a class's
+    launches differ by side, e.g. the C3 direct kernel runs 187 ms in the item half and 69 us in
+    the user half), that launch's algorithmic flops and bytes over its
+    HIP-event time, the bound (MFMA when the launch's intensity is above the ridge, else HBM) and
+    the fraction of that peak."""
+    peak_tf = PEAK_F32_TFLOPS if precision == 32 else PEAK_F64_TFLOPS
+    ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
+    direct_name = "wals_big_kernel" if k > 128 else "wals_direct_kernel"
+    classes = {}
+    for cls, name in ((0, direct_name), (1, "wals_whitened (row solve + unwhiten)")):
+        tot = ctx.kernel_stats(cls)
+        if tot["launches"] == 0 or tot["ms"] <= 0:
+            continue
+        per = {}
+        for side in (0, 1):
+            st = ctx.kernel_stats_side(cls, side)
+            if st["launches"] and st["ms"] > 0:
+                n = st["launches"]
+                per[side] = dict(launch_ms=st["ms"] / n, flops=st["flops"] / n, bytes=st["bytes"] / n)
+        side = max(per, key=lambda sd: per[sd]["launch_ms"])
+        p = per[side]
+        sec = p["launch_ms"] / 1e3
+        tf, gbs = p["flops"] / sec / 1e12, p["bytes"] / sec / 1e9
+        if p["flops"] / p["bytes"] >= ridge:
+            bound, ach, pk, unit = "mfma", tf, peak_tf, "TFLOP/s"
+        else:
+            bound, ach, pk, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
+        classes[name] = dict(side=side, launch_ms=round(p["launch_ms"], 3), bound=bound,
+                             achieved=round(ach, 3), peak=pk, unit=unit, frac=round(ach / pk, 4),
+                             tflops=round(tf, 3), gbs=round(gbs, 1), flops_per_launch=p["flops"],
+                             bytes_per_launch=p["bytes"], total_ms=round(tot["ms"], 3),
+                             launches=tot["launches"],
+                             per_side_launch_ms={sd: round(v["launch_ms"], 3) for sd, v in per.items()})
+    return classes
 
 
 T_START = time.time()
@@ -509,37 +549,25 @@ def main():
     ms_epoch = el / args.steps * 1e3
     solves = (nu + ni) * args.steps
     value = solves / el
-    peak_tf = PEAK_F32_TFLOPS if args.precision == 32 else PEAK_F64_TFLOPS
-    ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
-    classes = {}
-    # direct rows: the one-wave kernel up to k = 128 (fp32 and fp64), the multi-wave one above
-    direct_name = "wals_big_kernel" if k > 128 else "wals_direct_kernel"
-    for cls, name in ((0, direct_name), (1, "wals_whitened (row solve + unwhiten)")):
-        ks = ctx.kernel_stats(cls)
-        if ks["launches"] == 0 or ks["ms"] <= 0:
-            continue
-        sec = ks["ms"] / 1e3 / ks["launches"]
-        fl = ks["flops"] / ks["launches"]
-        by = ks["bytes"] / ks["launches"]
-        classes[name] = dict(launch_ms=round(sec * 1e3, 3), tflops=round(fl / sec / 1e12, 3),
-                             gbs=round(by / sec / 1e9, 1), flops_per_launch=fl,
-                             bytes_per_launch=by, total_ms=round(ks["ms"], 3))
+    classes = roofline_classes(ctx, k, args.precision)
+    # the dominant class (most kernel time) carries the line's roofline; the class furthest
+    # below its own roofline is named beside it
     dom = max(classes, key=lambda n: classes[n]["total_ms"])
+    weak = min(classes, key=lambda n: classes[n]["frac"])
     d = classes[dom]
-    if d["flops_per_launch"] / d["bytes_per_launch"] >= ridge:
-        roof = {"kernel": dom, "bound": "mfma", "achieved": d["tflops"], "peak": peak_tf,
-                "unit": "TFLOP/s", "frac": round(d["tflops"] / peak_tf, 4)}
-    else:
-        roof = {"kernel": dom, "bound": "hbm", "achieved": d["gbs"], "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(d["gbs"] / PEAK_HBM_GBS, 4)}
-    # per-dispatch means over the profiled run, like `achieved` (mean bytes per launch)
+    roof = {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
+            "unit": d["unit"], "frac": d["frac"], "launch_ms": d["launch_ms"],
+            "launch_side": d["side"],
+            "weakest": {"kernel": weak, "bound": classes[weak]["bound"],
+                        "frac": classes[weak]["frac"], "launch_ms": classes[weak]["launch_ms"]}}
+    # PMC bytes of the same (large) launch, from the newest committed summary for this workload
     traffic, tsrc = pmc_traffic(args.config, args.precision, dom, k)
     roof.update({"traffic": round(traffic, 0) if traffic else None,
                  "traffic_algorithmic_ratio": round(traffic / d["bytes_per_launch"], 3) if traffic else None,
-                 # the counted L2↔fabric bytes per launch over this run's launch time (MALL hits
+                 # the counted L2<->fabric bytes per launch over this run's launch time (MALL hits
                  # included: the fabric rate the class runs at)
                  "traffic_gbs": round(traffic / (d["launch_ms"] / 1e3) / 1e9, 1) if traffic else None,
-                 "traffic_source": tsrc, "launch_ms": d["launch_ms"], "classes": classes})
+                 "traffic_source": tsrc, "classes": classes})
     half = ctx.kernel_stats(2)
     epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
     hbm_frac_epoch = epoch_bytes / (ms_epoch / 1e3) / (PEAK_HBM_GBS * 1e9)
@@ -571,7 +599,7 @@ def main():
     nthreads, host = cpu_share()
     if not args.no_parity and world == 1:
         t0 = time.perf_counter()
-        out["parity"] = parity_check(ctx, CONFIGS[args.config], nthreads)
+        out["parity"] = parity_check(ctx, CONFIGS[args.config], nthreads, args.precision)
         log("parity check %.1fs: %s" % (time.perf_counter() - t0, out["parity"]))
     if args.cpu_baseline != "none" and world == 1:
         cfg = (nu, ni, nnz, k, seed)

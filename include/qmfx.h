@@ -76,9 +76,10 @@ int qmfx_gen_synthetic(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t nn
  * is qmfx_gen_synthetic.  *nnz_out = unique pairs kept. */
 int qmfx_gen_synthetic_zipf(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t ndraws,
                             uint64_t seed, double zipf_s, int64_t* nnz_out);
-/* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data). */
+/* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data).  values are
+ * returned in double, exactly as the device holds them (an fp32 context's values widened). */
 int qmfx_download_csr(qmfx_ctx* ctx, int side, int64_t* rowptr, int32_t* colidx,
-                      float* values);
+                      double* values);
 
 /* ---- factors (FactorData.h) ------------------------------------------------------------- */
 int qmfx_set_factors(qmfx_ctx* ctx, int side, const double* rowmajor);
@@ -185,6 +186,10 @@ int qmfx_solve_kernel_stats(qmfx_ctx* ctx, double* total_ms, int64_t* launches,
  * bytes are the algorithmic work of that class (SURVEY.md §8(d) accounting). */
 int qmfx_kernel_stats(qmfx_ctx* ctx, int cls, double* total_ms, int64_t* launches,
                       double* flops, double* bytes);
+/* qmfx_kernel_stats restricted to the halves that solved `side` (0 users, 1 items): a class's
+ * launches differ by side, so the per-launch time of the class's large launch is read here. */
+int qmfx_kernel_stats_side(qmfx_ctx* ctx, int cls, int side, double* total_ms, int64_t* launches,
+                           double* flops, double* bytes);
 int qmfx_reset_stats(qmfx_ctx* ctx);
 
 /* ---- self tests ------------------------------------------------------------------------------ */

@@ -18,7 +18,6 @@ _lib = None
 c_i64p = ctypes.POINTER(ctypes.c_int64)
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_f64p = ctypes.POINTER(ctypes.c_double)
-c_f32p = ctypes.POINTER(ctypes.c_float)
 
 
 def build():
@@ -36,8 +35,8 @@ def lib():
         L.orc_wals_create.argtypes = [c_i64p, c_i64p, c_f64p, ctypes.c_int64, ctypes.c_int,
                                       ctypes.c_double, ctypes.c_double]
         L.orc_wals_create_csr.restype = vp
-        L.orc_wals_create_csr.argtypes = [ctypes.c_int64, ctypes.c_int64, c_i64p, c_i32p, c_f32p,
-                                          c_i64p, c_i32p, c_f32p, ctypes.c_int,
+        L.orc_wals_create_csr.argtypes = [ctypes.c_int64, ctypes.c_int64, c_i64p, c_i32p, c_f64p,
+                                          c_i64p, c_i32p, c_f64p, ctypes.c_int,
                                           ctypes.c_double, ctypes.c_double]
         L.orc_wals_destroy.argtypes = [vp]
         for f in ("orc_wals_nusers", "orc_wals_nitems", "orc_wals_nnz"):
@@ -58,7 +57,7 @@ def lib():
         L.orc_linear_symmetric_solve.restype = ctypes.c_int
         L.orc_linear_symmetric_solve.argtypes = [c_f64p, c_f64p, ctypes.c_int]
         L.orc_solve_rows.restype = ctypes.c_int
-        L.orc_solve_rows.argtypes = [c_f64p, ctypes.c_int64, ctypes.c_int, c_i64p, c_i32p, c_f32p,
+        L.orc_solve_rows.argtypes = [c_f64p, ctypes.c_int64, ctypes.c_int, c_i64p, c_i32p, c_f64p,
                                      c_i64p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_int, c_f64p, c_f64p]
         L.orc_update_one.restype = ctypes.c_double
@@ -116,12 +115,12 @@ class OracleWALS:
         L = lib()
         self.k = int(nfactors)
         arrs = [np.ascontiguousarray(urp, np.int64), np.ascontiguousarray(ucol, np.int32),
-                np.ascontiguousarray(uval, np.float32), np.ascontiguousarray(irp, np.int64),
-                np.ascontiguousarray(icol, np.int32), np.ascontiguousarray(ival, np.float32)]
+                np.ascontiguousarray(uval, np.float64), np.ascontiguousarray(irp, np.int64),
+                np.ascontiguousarray(icol, np.int32), np.ascontiguousarray(ival, np.float64)]
         self._keep = arrs
         self.h = L.orc_wals_create_csr(nusers, nitems, _p(arrs[0], c_i64p), _p(arrs[1], c_i32p),
-                                       _p(arrs[2], c_f32p), _p(arrs[3], c_i64p),
-                                       _p(arrs[4], c_i32p), _p(arrs[5], c_f32p), self.k,
+                                       _p(arrs[2], c_f64p), _p(arrs[3], c_i64p),
+                                       _p(arrs[4], c_i32p), _p(arrs[5], c_f64p), self.k,
                                        float(lam), float(alpha))
         return self
 
@@ -226,13 +225,13 @@ def solve_rows(Y, rowptr, col, val, rows, alpha, lam, nthreads=1):
     Y = np.ascontiguousarray(Y, np.float64)
     rowptr = np.ascontiguousarray(rowptr, np.int64)
     col = np.ascontiguousarray(col, np.int32)
-    val = np.ascontiguousarray(val, np.float32)
+    val = np.ascontiguousarray(val, np.float64)
     rows = np.ascontiguousarray(rows, np.int64)
     k = Y.shape[1]
     x = np.empty((len(rows), k), np.float64)
     loss = np.empty(len(rows), np.float64)
     info = lib().orc_solve_rows(_p(Y, c_f64p), Y.shape[0], k, _p(rowptr, c_i64p), _p(col, c_i32p),
-                                _p(val, c_f32p), _p(rows, c_i64p), len(rows), float(alpha),
+                                _p(val, c_f64p), _p(rows, c_i64p), len(rows), float(alpha),
                                 float(lam), int(nthreads), _p(x, c_f64p), _p(loss, c_f64p))
     if info != 0:
         raise RuntimeError("dsysv info=%d" % info)

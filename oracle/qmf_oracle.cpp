@@ -425,8 +425,8 @@ void* orc_wals_create(const int64_t* uid, const int64_t* iid, const double* val,
 // baseline on device-generated synthetic data).  Signals keep the CSR order, which is
 // ascending column index = ascending id, exactly as groupSignals would produce.
 void* orc_wals_create_csr(int64_t nusers, int64_t nitems, const int64_t* urowptr,
-                          const int32_t* ucol, const float* uval, const int64_t* irowptr,
-                          const int32_t* icol, const float* ival, int k, double lambda,
+                          const int32_t* ucol, const double* uval, const int64_t* irowptr,
+                          const int32_t* icol, const double* ival, int k, double lambda,
                           double alpha) {
   auto* w = new Wals();
   w->k = k;
@@ -438,13 +438,13 @@ void* orc_wals_create_csr(int64_t nusers, int64_t nitems, const int64_t* urowptr
   for (int64_t u = 0; u < nusers; ++u) {
     w->userSignals[u].sourceId = u;
     for (int64_t e = urowptr[u]; e < urowptr[u + 1]; ++e)
-      w->userSignals[u].group.push_back(Signal{ucol[e], (double)uval[e]});
+      w->userSignals[u].group.push_back(Signal{ucol[e], uval[e]});
   }
   w->itemSignals.resize(nitems);
   for (int64_t i = 0; i < nitems; ++i) {
     w->itemSignals[i].sourceId = i;
     for (int64_t e = irowptr[i]; e < irowptr[i + 1]; ++e)
-      w->itemSignals[i].group.push_back(Signal{icol[e], (double)ival[e]});
+      w->itemSignals[i].group.push_back(Signal{icol[e], ival[e]});
   }
   w->U.assign((size_t)nusers * k, 0.0);
   w->I.assign((size_t)nitems * k, 0.0);
@@ -600,7 +600,7 @@ double orc_update_one(const double* Y, int64_t nY, int k, const int64_t* cols,
 // only by rounding).  Writes x (nrows×k) and the row losses.  Returns the first nonzero
 // dsysv info, or 0.
 int orc_solve_rows(const double* Y, int64_t nY, int k, const int64_t* rowptr,
-                   const int32_t* col, const float* val, const int64_t* rows, int64_t nrows,
+                   const int32_t* col, const double* val, const int64_t* rows, int64_t nrows,
                    double alpha, double lambda, int nthreads, double* x_out, double* loss_out) {
   if (nthreads < 1) nthreads = 1;
   std::vector<double> y(Y, Y + (size_t)nY * k);
@@ -631,7 +631,7 @@ int orc_solve_rows(const double* Y, int64_t nY, int k, const int64_t* rowptr,
         const int64_t r = rows[q];
         SignalGroup sg{r, {}};
         for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e)
-          sg.group.push_back(Signal{col[e], (double)val[e]});
+          sg.group.push_back(Signal{col[e], val[e]});
         int info = 0;
         loss_out[q] = updateFactorsForOne(X, one, y, ident, sg, YtY, alpha, lambda, k, &info);
         if (info) infos[(size_t)t] = info;

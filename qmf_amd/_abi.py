@@ -35,7 +35,7 @@ SIGNATURES = {
     "qmfx_upload_csr": [vp, c_int, P_i64, P_i32, P_f64, c_i64],
     "qmfx_gen_synthetic": [vp, c_i64, c_i64, c_i64, c_u64, P_i64],
     "qmfx_gen_synthetic_zipf": [vp, c_i64, c_i64, c_i64, c_u64, c_dbl, P_i64],
-    "qmfx_download_csr": [vp, c_int, P_i64, P_i32, P_f32],
+    "qmfx_download_csr": [vp, c_int, P_i64, P_i32, P_f64],
     "qmfx_group_signals": [vp, vp, c_i64, P_i64, P_i64],
     "qmfx_get_ids": [vp, c_int, P_i64],
     "qmfx_set_factors": [vp, c_int, P_f64],
@@ -63,6 +63,7 @@ SIGNATURES = {
     "qmfx_wals_half_multi": [ctypes.POINTER(vp), c_int, c_int, c_dbl, c_dbl, P_f64],
     "qmfx_solve_kernel_stats": [vp, P_f64, P_i64, P_f64, P_f64],
     "qmfx_kernel_stats": [vp, c_int, P_f64, P_i64, P_f64, P_f64],
+    "qmfx_kernel_stats_side": [vp, c_int, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_reset_stats": [vp],
     "qmfx_selftest_mfma": [c_int, c_int, P_f64, P_f64, P_f64],
 }
@@ -243,8 +244,8 @@ class Context:
         n = nu if side == 0 else ni
         rp = np.empty(n + 1, np.int64)
         col = np.empty(max(nnz, 1), np.int32)
-        val = np.empty(max(nnz, 1), np.float32)
-        _check(lib().qmfx_download_csr(self.h, side, _p(rp, P_i64), _p(col, P_i32), _p(val, P_f32)))
+        val = np.empty(max(nnz, 1), np.float64)  # exactly the device's values (fp32 widened)
+        _check(lib().qmfx_download_csr(self.h, side, _p(rp, P_i64), _p(col, P_i32), _p(val, P_f64)))
         return rp, col[:nnz], val[:nnz]
 
     # ---- factors
@@ -374,6 +375,13 @@ class Context:
         ms, n, fl, by = c_dbl(), c_i64(), c_dbl(), c_dbl()
         _check(lib().qmfx_kernel_stats(self.h, cls, ctypes.byref(ms), ctypes.byref(n),
                                        ctypes.byref(fl), ctypes.byref(by)))
+        return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
+
+    def kernel_stats_side(self, cls, side):
+        """kernel_stats(cls) over the halves that solved `side` only."""
+        ms, n, fl, by = c_dbl(), c_i64(), c_dbl(), c_dbl()
+        _check(lib().qmfx_kernel_stats_side(self.h, cls, side, ctypes.byref(ms), ctypes.byref(n),
+                                            ctypes.byref(fl), ctypes.byref(by)))
         return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
 
     def reset_stats(self):

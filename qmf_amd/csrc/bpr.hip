@@ -48,8 +48,11 @@ __device__ __forceinline__ void store_row(const Row<T, E>& r, T* base, int lane,
     if (lane + 64 * e < kp) st_shared(base + lane + 64 * e, r.v[e]);
 }
 // Adds (r − r0) to the shared row with L2 atomics: a concurrent wave's update of the same row
-// is kept instead of being overwritten (Hogwild without lost updates; the C4 "wavefront-atomic"
-// SGD).  Only the read that formed the gradient can be stale, as in the reference's threads.
+// is kept instead of being overwritten (the C4 "wavefront-atomic" SGD).  Used for the item
+// rows, and for the user row when some user is heavy (BprArgs::atomic_user); otherwise the
+// user row is stored plainly and a rare concurrent update of one user is overwritten, as with
+// the reference's unsynchronised threads.  Only the read that formed the gradient can be
+// stale, as in the reference's threads.
 template <typename T, int E>
 __device__ __forceinline__ void add_row(const Row<T, E>& r, const Row<T, E>& r0, T* base,
                                         int lane, int kp) {
@@ -178,7 +181,8 @@ __device__ __forceinline__ int64_t draw_negative_t(const A& a, const int32_t* it
 // and q_p are loaded once and carried through the steps, as one thread of the reference
 // sees its own writes (BPREngine::update :178-220 per step); the negatives are drawn first
 // and their rows loaded together (a repeated negative takes the updated row of its earlier
-// draw).  Each row's net change is added to memory after its last update (add_row).
+// draw).  Each item row's net change is added to memory after its last update (add_row);
+// the user row is stored (or added, for heavy users) at the end.
 template <typename T, int E>
 __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int64_t p,
                                              const int64_t (&n)[4], int nn, int lane) {
@@ -251,12 +255,16 @@ __device__ __forceinline__ bool bpr_positive(const BprArgs<T>& a, int64_t u, int
       if (a.use_biases && lane == 0) unsafeAtomicAdd(a.bias + n[j], bn[j] - bn0[j]);
     }
   }
-  // the user row with a plain (relaxed, L2-coherent) store: with ≥ 16× more users than
-  // concurrent waves two waves rarely hold the same user (C4: ≈0.4% of positives), and an
-  // overwrite then is exactly the reference's Hogwild store; the item rows keep the atomic
-  // adds (100K items under 4096 waves collide often).  One of five atomic rows per positive
-  // fewer: the epoch is bound by the ≈1.3 TB/s chip-wide float-atomic rate.
-  store_row(pu, a.U + u * kp, lane, kp);
+  // the user row with a plain (relaxed, L2-coherent) store while two waves rarely hold the
+  // same user: the host sets atomic_user when the heaviest user's share of the positives
+  // times the concurrent waves exceeds 1% (C4's uniform users: ≈0.4%), and an overwrite is
+  // then exactly the reference's Hogwild store; the item rows keep the atomic adds (100K
+  // items under 4096 waves collide often).  One of five atomic rows per positive fewer: the
+  // epoch is bound by the ≈1.3 TB/s chip-wide float-atomic rate.
+  if (a.atomic_user)
+    add_row(pu, pu0, a.U + u * kp, lane, kp);
+  else
+    store_row(pu, a.U + u * kp, lane, kp);
   add_row(qp, qp0, a.I + p * kp, lane, kp);
   if (a.use_biases && lane == 0) unsafeAtomicAdd(a.bias + p, bp - bp0);
   return ok;

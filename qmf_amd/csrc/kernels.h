@@ -186,6 +186,7 @@ struct BprArgs {
   int kp;                  // row stride (padded factors)
   int32_t* bad;            // set to 1 if a derivative was not finite
   int waves;               // concurrent waves of the epoch kernel (Hogwild width)
+  int atomic_user;         // 1: add the user row's net change atomically (heavy users)
 };
 
 hipError_t launch_bpr_epoch_f32(const BprArgs<float>& a, int kp, hipStream_t s);

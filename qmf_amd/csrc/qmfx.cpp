@@ -136,6 +136,7 @@ struct qmfx_ctx {
   int64_t* pos_user = nullptr;
   int32_t* pos_item = nullptr;
   int64_t npos = 0;
+  int64_t max_user_pos = 0;  // largest positive count of one user (Hogwild collision estimate)
   int64_t* urowptr = nullptr;
   int32_t* uitems = nullptr;
   void* bias = nullptr;
@@ -196,6 +197,12 @@ struct qmfx_ctx {
   hipStream_t comm_stream = nullptr;
   double cls_ms[3] = {0, 0, 0}, cls_flops[3] = {0, 0, 0}, cls_bytes[3] = {0, 0, 0};
   int64_t cls_launches[3] = {0, 0, 0};
+  // the same per solved side (a class's launches differ by side: at C3 the direct kernel
+  // takes 187 ms in the item half and 69 µs in the user half)
+  double side_ms[2][3] = {}, side_flops[2][3] = {}, side_bytes[2][3] = {};
+  // set when qmfx_wals_half_multi aborted the clique after a failed collective
+  bool comm_aborted = false;
+  int64_t side_launches[2][3] = {};
 };
 
 namespace {
@@ -374,6 +381,8 @@ int build_buckets(qmfx_ctx* c, int side) {
     std::vector<std::pair<int64_t, int64_t>> direct;
     for (int64_t r = pc.rb; r < pc.re; ++r) {
       const int64_t n = sb.h_rowptr[r + 1] - sb.h_rowptr[r];
+      // RowDesc::n is int32 (segments too: seg_len is clamped at create)
+      if (n > INT32_MAX) return fail("a row with more than 2^31-1 signals is not supported");
       const int64_t ntn = (std::max<int64_t>(n, 1) + 15) / 16;
       if (ntn <= mx) {
         wlist[ntn - 1].push_back(r);
@@ -564,7 +573,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
   c->ksel = read_kernel_sel();
   if (const char* hm = std::getenv("QMFX_HEAVY_MIN")) c->heavy_min = std::max<int64_t>(std::atoll(hm), 0);
-  if (const char* sl = std::getenv("QMFX_SEG_LEN")) c->seg_len = std::max<int64_t>(std::atoll(sl), 64);
+  if (const char* sl = std::getenv("QMFX_SEG_LEN"))
+    c->seg_len = std::min<int64_t>(std::max<int64_t>(std::atoll(sl), 64), INT32_MAX);
   if (const char* np = std::getenv("QMFX_PIECES"))
     c->npieces = std::min(std::max(std::atoi(np), 1), QMFX_MAX_PIECES);
   hipError_t e = hipSetDevice(device);
@@ -797,7 +807,7 @@ int qmfx_get_ids(qmfx_ctx* c, int side, int64_t* ids) {
   return 0;
 }
 
-int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, float* values) {
+int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, double* values) {
   SideBuf& sb = c->s[side];
   if (!sb.rowptr) return fail("no CSR for this side");
   if (sb.sharded) return fail("the CSR is sharded over ranks (qmfx_dist_init): only this rank's rows are held");
@@ -806,12 +816,13 @@ int qmfx_download_csr(qmfx_ctx* c, int side, int64_t* rowptr, int32_t* colidx, f
   HIPCHK(scopy(c, rowptr, sb.rowptr, (size_t)(sb.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
   if (sb.nnz > 0) {
     HIPCHK(scopy(c, colidx, sb.col, (size_t)sb.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (c->prec == 32) {
-      HIPCHK(scopy(c, values, sb.val, (size_t)sb.nnz * 4, hipMemcpyDeviceToHost));
+    if (c->prec == 64) {
+      HIPCHK(scopy(c, values, sb.val, (size_t)sb.nnz * 8, hipMemcpyDeviceToHost));
     } else {
-      std::vector<double> v((size_t)sb.nnz);
-      HIPCHK(scopy(c, v.data(), sb.val, (size_t)sb.nnz * 8, hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < v.size(); ++i) values[i] = (float)v[i];
+      // fp32 context: the device holds float values; widen exactly
+      std::vector<float> v((size_t)sb.nnz);
+      HIPCHK(scopy(c, v.data(), sb.val, (size_t)sb.nnz * 4, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < v.size(); ++i) values[i] = (double)v[i];
     }
   }
   return 0;
@@ -943,6 +954,8 @@ int half_begin(qmfx_ctx* c, int side, double alpha, double lambda) {
   SideBuf& R = c->s[1 - side];
   if (!L.rowptr) return fail("no interactions uploaded for the solved side");
   if (!L.buckets_valid) return fail("row buckets not built");
+  if (c->comm_aborted)
+    return fail("the RCCL clique was aborted after a failed collective; recreate the contexts");
   if (set_dev(c)) return -2;
   if (int rc = ensure_side_factors(c, side)) return rc;
   if (int rc = ensure_side_factors(c, 1 - side)) return rc;
@@ -1084,6 +1097,9 @@ int half_piece(qmfx_ctx* c, int j) {
 // piece j of this rank → every rank (one ncclGroup; nests inside a caller's group)
 int half_comm_piece(qmfx_ctx* c, int j) {
   if (set_dev(c)) return -2;
+  // fault injection for the clique's failure path (tests): QMFX_FAULT_COMM_RANK=<rank>
+  if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK"))
+    if (c->comm && std::atoi(f) == c->rank) return fail("injected collective failure", -3);
   SideBuf& L = c->s[c->hs.side];
   const int P = (int)L.pieces.size();
   if (c->comm) {
@@ -1166,6 +1182,17 @@ int half_end(qmfx_ctx* c, double* loss_sum) {
   }
   HIPCHK(hipEventElapsedTime(&ms_h, c->evh[0], c->evh[2]));
   const double k = c->k, s = (double)c->esz;
+  const int sd = c->hs.side;
+  auto acc = [&](int cls, double ms, double fl, double by) {
+    c->cls_ms[cls] += ms;
+    c->cls_launches[cls] += 1;
+    c->cls_flops[cls] += fl;
+    c->cls_bytes[cls] += by;
+    c->side_ms[sd][cls] += ms;
+    c->side_launches[sd][cls] += 1;
+    c->side_flops[sd][cls] += fl;
+    c->side_bytes[sd][cls] += by;
+  };
   const bool use_w = c->hs.use_w;
   const int64_t nD = c->hs.nD, nW = L.wb[kMaxNTN];
   const double nzd = use_w ? L.nnz_d : L.nnz_d + L.nnz_w, nd = (double)nD;
@@ -1174,25 +1201,16 @@ int half_end(qmfx_ctx* c, double* loss_sum) {
   if (nD > 0) {
     fl_d = nzd * k * (k + 1) + nzd * 2 * k + nd * (k * k * k / 3.0 + 2 * k * k);
     by_d = nzd * (4 + s) + nzd * k * s + nd * k * s + (nd + 1) * 8;
-    c->cls_ms[0] += ms_d;
-    c->cls_launches[0] += 1;
-    c->cls_flops[0] += fl_d;
-    c->cls_bytes[0] += by_d;
+    acc(0, ms_d, fl_d, by_d);
   }
   if (nW > 0 && use_w) {
     // whitened-row flops precomputed per side in build_buckets; bytes: gathers, x' write,
     // x' read + x write
     fl_w = L.flops_w;
     by_w = nzw * (4 + s) + nzw * k * s + nw * k * s * 3 + nw * 16;
-    c->cls_ms[1] += ms_w;
-    c->cls_launches[1] += 1;
-    c->cls_flops[1] += fl_w;
-    c->cls_bytes[1] += by_w;
+    acc(1, ms_w, fl_w, by_w);
   }
-  c->cls_ms[2] += ms_h;
-  c->cls_launches[2] += 1;
-  c->cls_flops[2] += fl_d + fl_w;
-  c->cls_bytes[2] += by_d + by_w;
+  acc(2, ms_h, fl_d + fl_w, by_d + by_w);
   c->solve_ms += ms_d + ms_w;
   c->solve_launches += 1;
   c->solve_flops += fl_d + fl_w;
@@ -1236,25 +1254,41 @@ int qmfx_wals_half_multi(qmfx_ctx* const* ctxs, int n, int side, double alpha, d
   const int P = (int)ctxs[0]->s[side].pieces.size();
   for (int i = 1; i < n; ++i)
     if ((int)ctxs[i]->s[side].pieces.size() != P) return fail("contexts disagree on the pieces");
+  // A context that fails after others have posted their part of a group would leave those
+  // collectives waiting for peers that never join, and the next sync would hang: abort every
+  // communicator of the clique instead (outstanding collectives are cancelled), so the call
+  // returns the error and later calls on these contexts fail loudly.
+  auto abort_clique = [&](int rc) {
+    for (int i = 0; i < n; ++i) {
+      if (ctxs[i]->comm) {
+        (void)ncclCommAbort(ctxs[i]->comm);
+        ctxs[i]->comm = nullptr;
+        ctxs[i]->comm_aborted = true;
+      }
+    }
+    return rc;
+  };
   for (int j = 0; j < P; ++j) {
     for (int i = 0; i < n; ++i)
-      if (int rc = half_piece(ctxs[i], j)) return rc;
+      if (int rc = half_piece(ctxs[i], j)) return abort_clique(rc);
     // one thread drives every communicator: all ranks' broadcasts of piece j in one group
     NCCLCHK(ncclGroupStart());
     int rc = 0;
     for (int i = 0; i < n && rc == 0; ++i) rc = half_comm_piece(ctxs[i], j);
-    NCCLCHK(ncclGroupEnd());
-    if (rc) return rc;
+    const ncclResult_t ge = ncclGroupEnd();
+    if (rc) return abort_clique(rc);
+    if (ge != ncclSuccess) return abort_clique(fail(std::string("RCCL: ") + ncclGetErrorString(ge), -4));
   }
   for (int i = 0; i < n; ++i)
-    if (int rc = half_tail(ctxs[i])) return rc;
+    if (int rc = half_tail(ctxs[i])) return abort_clique(rc);
   {
     NCCLCHK(ncclGroupStart());
     int rc = 0;
     for (int i = 0; i < n && rc == 0; ++i)
       if (ctxs[i]->comm) rc = half_comm_status(ctxs[i]);
-    NCCLCHK(ncclGroupEnd());
-    if (rc) return rc;
+    const ncclResult_t ge = ncclGroupEnd();
+    if (rc) return abort_clique(rc);
+    if (ge != ncclSuccess) return abort_clique(fail(std::string("RCCL: ") + ncclGetErrorString(ge), -4));
   }
   double first = 0.0;
   for (int i = 0; i < n; ++i) {
@@ -1392,6 +1426,8 @@ int qmfx_bpr_set_positives(qmfx_ctx* c, const int64_t* users, const int64_t* ite
     rp[keys[e] / ni + 1]++;
     ui[e] = (int32_t)(keys[e] % ni);
   }
+  c->max_user_pos = 0;
+  for (int64_t u = 0; u < nu; ++u) c->max_user_pos = std::max(c->max_user_pos, rp[u + 1]);
   for (int64_t u = 0; u < nu; ++u) rp[u + 1] += rp[u];
   HIPCHK(hipMalloc(&c->urowptr, (size_t)(nu + 1) * 8));
   HIPCHK(hipMalloc(&c->uitems, ui.size() * 4));
@@ -1473,6 +1509,12 @@ static BprArgs<T> bpr_args(qmfx_ctx* c, double lr, double bl, double ul, double 
   // default does).
   const int64_t rows = std::min(c->s[0].n, c->s[1].n);
   a.waves = (int)std::max<int64_t>(1, std::min<int64_t>({4096, rows / 16, std::max<int64_t>(c->npos, 1)}));
+  // The user row is stored plainly (an overwrite is the reference's Hogwild store) only while
+  // two waves rarely hold the same user: the heaviest user's share of the positives times
+  // the concurrent waves is the chance that another wave holds that user at a given moment.
+  // Above 1% (skewed user activity) its net change is added atomically like the item rows.
+  a.atomic_user = (double)a.waves * (double)c->max_user_pos > 0.01 * (double)std::max<int64_t>(c->npos, 1) ? 1 : 0;
+  if (const char* f = std::getenv("QMFX_BPR_ATOMIC_USER")) a.atomic_user = std::atoi(f) ? 1 : 0;
   return a;
 }
 
@@ -1815,12 +1857,27 @@ int qmfx_kernel_stats(qmfx_ctx* c, int cls, double* total_ms, int64_t* launches,
   return 0;
 }
 
+int qmfx_kernel_stats_side(qmfx_ctx* c, int cls, int side, double* total_ms, int64_t* launches,
+                           double* flops, double* bytes) {
+  if (cls < 0 || cls > 2) return fail("class must be 0 (direct), 1 (whitened) or 2 (half)");
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  if (total_ms) *total_ms = c->side_ms[side][cls];
+  if (launches) *launches = c->side_launches[side][cls];
+  if (flops) *flops = c->side_flops[side][cls];
+  if (bytes) *bytes = c->side_bytes[side][cls];
+  return 0;
+}
+
 int qmfx_reset_stats(qmfx_ctx* c) {
   c->solve_ms = c->solve_flops = c->solve_bytes = 0;
   c->solve_launches = 0;
   for (int i = 0; i < 3; ++i) {
     c->cls_ms[i] = c->cls_flops[i] = c->cls_bytes[i] = 0;
     c->cls_launches[i] = 0;
+    for (int sd = 0; sd < 2; ++sd) {
+      c->side_ms[sd][i] = c->side_flops[sd][i] = c->side_bytes[sd][i] = 0;
+      c->side_launches[sd][i] = 0;
+    }
   }
   return 0;
 }

@@ -55,3 +55,13 @@ def test_create_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(qmf_amd.QmfxError):
         qmf_amd.Context(8, 32)
+
+
+def test_download_csr_is_double_across_the_abi():
+    # qmfx_download_csr hands values back in double (an fp32 context's widened exactly), so
+    # host-side checkers never see an fp32-narrowed problem
+    src = open(os.path.join(ROOT, "include", "qmfx.h")).read()
+    decl = re.search(r"int qmfx_download_csr\(([^)]*)\)", src).group(1)
+    assert "double* values" in decl and "float" not in decl
+    import ctypes
+    assert qmf_amd._abi.SIGNATURES["qmfx_download_csr"][-1] is ctypes.POINTER(ctypes.c_double)

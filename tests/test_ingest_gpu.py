@@ -30,8 +30,9 @@ def check_exact(users, items, values, precision=64):
     for (rp, col, val), (xrp, xcol, xval) in zip(csr, (ru, ri)):
         assert np.array_equal(rp, xrp)
         assert np.array_equal(col, xcol)
-        # download_csr returns values as fp32; the inputs here are fp32-exact
-        assert np.array_equal(val, xval.astype(np.float32))
+        # download_csr returns the device's values in double (an fp32 context's widened)
+        assert val.dtype == np.float64
+        assert np.array_equal(val, xval if precision == 64 else xval.astype(np.float32).astype(np.float64))
     return uids, iids, csr
 
 
@@ -86,3 +87,17 @@ def test_ingest_millions():
     items = rng.zipf(1.3, n) % 50_000
     values = rng.integers(1, 6, n).astype(np.float64)
     check_exact(users, items, values, precision=32)
+
+
+@pytest.mark.parametrize("precision", [32, 64])
+def test_download_csr_returns_device_values_in_double(precision):
+    # real-valued weights (not fp32-exact): an fp64 context hands back exactly its doubles,
+    # an fp32 context its floats widened -- what bench.py's parity check and CPU baseline
+    # feed the oracle, so they solve the device's own problem
+    rng = np.random.default_rng(23)
+    n = 20_000
+    users = rng.integers(0, 3000, n)
+    items = rng.integers(0, 700, n)
+    values = rng.uniform(0.1, 5.0, n)
+    check_exact(users, items, values, precision)
+    assert not np.array_equal(values, values.astype(np.float32).astype(np.float64))

@@ -165,3 +165,31 @@ def test_distribution_file_short_file(tmp_path):
     p.write_text("0.5\n0.25\n-1\n")
     assert o.load_distribution_file(str(p)) == 3
     np.testing.assert_array_equal(o.factors(1), [[0.5, 0.25], [-1, 0], [0, 0]])
+
+
+def test_csr_entry_points_keep_double_values():
+    # The full-size parity check and the CPU baseline build the oracle from the device's
+    # downloaded CSR (qmfx_download_csr returns double).  On real-valued (non-fp32-exact)
+    # weights, the CSR constructor and solve_rows must see exactly those doubles: the same
+    # factors as the triple-based init (WALSEngine::init) on the same data, bit for bit.
+    rng = np.random.default_rng(5)
+    nu, ni, k = 40, 30, 8
+    pairs = np.unique(rng.integers(0, nu * ni, 500))
+    u, i = pairs // ni, pairs % ni
+    v = rng.uniform(0.1, 5.0, len(pairs))
+    assert not np.array_equal(v, v.astype(np.float32).astype(np.float64))
+    a = po.OracleWALS(u, i, v, k)
+    assert a.nusers == nu and a.nitems == ni  # every id present: idx == id
+    urp, ucol, uval = a.csr(0)
+    irp, icol, ival = a.csr(1)
+    b = po.OracleWALS.from_csr(nu, ni, urp, ucol, uval, irp, icol, ival, k, 0.05, 40.0)
+    Y = rng.uniform(-0.5, 0.5, (ni, k))
+    a.set_factors(1, Y)
+    b.set_factors(1, Y)
+    la, lb = a.iterate(0), b.iterate(0)
+    assert la == lb and np.array_equal(a.factors(0), b.factors(0))
+    rows = np.arange(nu, dtype=np.int64)
+    x, _ = po.solve_rows(Y, urp, ucol.astype(np.int32), uval, rows, 40.0, 0.05)
+    x32, _ = po.solve_rows(Y, urp, ucol.astype(np.int32), uval.astype(np.float32), rows, 40.0, 0.05)
+    assert np.allclose(x, a.factors(0), rtol=1e-12, atol=1e-14)
+    assert not np.array_equal(x, x32)  # the fp32-narrowed problem is a different one

@@ -6,7 +6,9 @@
 run_counter_collection.csv.  FETCH_SIZE / WRITE_SIZE are in KiB; per MI355X_MICROARCH.md
 ("HBM [CDNA4]") gfx950's FETCH_SIZE counts exactly half the bytes of 16-B-per-lane
 reads, so fetch is doubled (`fetch_bytes`); WRITE_SIZE is exact for 16-B stores.  Values
-are per dispatch (mean over the dispatches of that kernel)."""
+are per dispatch: the mean over the dispatches of that kernel, and (`*_max`) the largest
+dispatch, which is the large launch of a kernel that runs in both halves with very different
+sizes (bench.py's roofline reads that one)."""
 import collections
 import csv
 import glob
@@ -31,8 +33,10 @@ def main(src, out):
         e = {"dispatches": max(len(v) for v in cs.values())}
         if "FETCH_SIZE" in d:
             e["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * 2
+            e["fetch_bytes_max"] = max(cs["FETCH_SIZE"]) * 1024 * 2
         if "WRITE_SIZE" in d:
             e["write_bytes"] = d["WRITE_SIZE"] * 1024
+            e["write_bytes_max"] = max(cs["WRITE_SIZE"]) * 1024
         for c, v in d.items():
             if c.startswith("SQ_") or c.startswith("GRBM"):
                 e[c] = v
