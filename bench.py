@@ -45,8 +45,10 @@ CONFIGS = {
     # C3 with Zipf(1.0) item popularity: 550M draws -> ~502M unique pairs; ~2400 items hold
     # more than 16K signals (the largest ~9.4M), ~690K items at most 128
     "c3z": (10_000_000, 1_000_000, 550_000_000, 128, 3),
+    # C5 with the same Zipf(1.0) item popularity: the split-K heavy rows at k = 256
+    "c5z": (10_000_000, 1_000_000, 550_000_000, 256, 3),
 }
-ZIPF = {"c3z": 1.0}
+ZIPF = {"c3z": 1.0, "c5z": 1.0}
 BPR_CONFIGS = {"c4"}
 LAM, ALPHA = 0.05, 40.0
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md

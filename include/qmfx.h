@@ -102,7 +102,8 @@ int qmfx_wals_half(qmfx_ctx* ctx, int side, double alpha, double lambda, double*
 int qmfx_wals_failed_rows(qmfx_ctx* ctx, int64_t* rows, int64_t cap, int64_t* count);
 /* The row plan of `side` on this rank (11 counts): [0..7] whitened rows in the n×n buckets
  * n ≤ 16·(i+1) (used when λ > 0), [8] direct k×k rows, [9] split-K heavy rows (more than
- * QMFX_HEAVY_MIN signals, default 16384; the one-wave direct tilings, k ≤ 128), [10] their
+ * QMFX_HEAVY_MIN signals, default 16384; every k: the one-wave direct tilings and the multi-wave
+ * k > 128 kernel), [10] their
  * segments (QMFX_SEG_LEN signals each, default 8192). */
 int qmfx_row_classes(qmfx_ctx* ctx, int side, int64_t* counts);
 /* Per-row loss terms of the last half (n_side values; the sum is *loss_sum). */

@@ -55,6 +55,15 @@ hipError_t launch_heavy_reduce(float* part, float* partb, double* partc, const i
 hipError_t launch_heavy_reduce(double* part, double* partb, double* partc, const int64_t* hseg,
                                int64_t h0, int64_t nh, const double* Gimg, int nt, hipStream_t s);
 
+// The same for the multi-wave k > 128 tilings (wals_big.hip): builds G + λI's tile image in
+// Gimg first (runtime tile count, no column permutation).
+hipError_t launch_heavy_reduce_big(float* part, float* partb, double* partc, const int64_t* hseg,
+                                   int64_t h0, int64_t nh, const float* G, float* Gimg, int nt,
+                                   int k, double lambda, hipStream_t s);
+hipError_t launch_heavy_reduce_big(double* part, double* partb, double* partc, const int64_t* hseg,
+                                   int64_t h0, int64_t nh, const double* G, double* Gimg, int nt,
+                                   int k, double lambda, hipStream_t s);
+
 // Per-row kernels take one workgroup per row (slot = row_begin + blockIdx.x).  A launch's
 // total thread count must fit 32 bits (10M rows × 512 threads does not), so rows go out in
 // chunks of at most 2^31 / threads workgroups.

@@ -169,7 +169,7 @@ struct qmfx_ctx {
     int64_t nD = 0;
     const char* trace_path = nullptr;
   } hs;
-  // split-K heavy rows (one-wave direct tilings): rows with more than heavy_min signals are
+  // split-K heavy rows (direct and multi-wave tilings): rows with more than heavy_min signals are
   // cut into segments of seg_len (QMFX_HEAVY_MIN / QMFX_SEG_LEN, read once at create;
   // heavy_min 0 = off); partials [segments][NTT·256 + KP] in the context precision + Σc/flag
   int64_t heavy_min = 16384;
@@ -367,9 +367,8 @@ int build_buckets(qmfx_ctx* c, int side) {
   order.reserve(sb.rend - sb.rbeg);
   sb.pieces.assign(P, SideBuf::Piece{});
   int64_t nw_total = 0;
-  // split-K heavy rows: only the one-wave direct tilings (the multi-wave k > 128 kernel keeps
-  // whole rows)
-  const int64_t hmin = use_big_rows(c) ? 0 : c->heavy_min;
+  // split-K heavy rows at every k (the multi-wave k > 128 kernel has segment modes too)
+  const int64_t hmin = c->heavy_min;
   std::vector<RowDesc> segs, heavy;
   std::vector<int64_t> hseg;
   for (int j = 0; j < P; ++j) {
@@ -1038,12 +1037,23 @@ int half_piece(qmfx_ctx* c, int j) {
     // each row's first segment, then the row solves from those images
     if (int rc = launch_direct_range(c, L, R, pc.s0, pc.ns, alpha, lambda, nullptr, 1))
       return rc;
-    if (fp32)
+    if (use_big_rows(c)) {
+      // multi-wave tilings: G + λI's image is built here (the direct kernels' Gimg is not)
+      if (fp32)
+        HIPCHK(launch_heavy_reduce_big((float*)c->part, (float*)c->partb, c->partc, L.d_hseg,
+                                       pc.h0, pc.nh, (const float*)c->G, (float*)c->Gimg, c->nt,
+                                       c->k, lambda, c->stream));
+      else
+        HIPCHK(launch_heavy_reduce_big((double*)c->part, (double*)c->partb, c->partc, L.d_hseg,
+                                       pc.h0, pc.nh, (const double*)c->G, (double*)c->Gimg,
+                                       c->nt, c->k, lambda, c->stream));
+    } else if (fp32) {
       HIPCHK(launch_heavy_reduce((float*)c->part, (float*)c->partb, c->partc, L.d_hseg, pc.h0,
                                  pc.nh, (const float*)c->Gimg, c->nt, c->stream));
-    else
+    } else {
       HIPCHK(launch_heavy_reduce((double*)c->part, (double*)c->partb, c->partc, L.d_hseg,
                                  pc.h0, pc.nh, (const double*)c->Gimg, c->nt, c->stream));
+    }
     if (int rc = launch_direct_range(c, L, R, pc.h0, pc.nh, alpha, lambda, nullptr, 2))
       return rc;
   }

@@ -374,7 +374,13 @@ __device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m
   l = uint2{pack_hi16(lo[0], lo[1]), pack_hi16(lo[2], lo[3])};
 }
 
-template <typename T, int NT>
+// MODE (compile time, as in the one-wave direct kernel): 0 = row solve; 1 = split-K segment
+// Gram (slot = segment of a.desc: the Gram of its signals from zero, written as tile images
+// + rhs + Σc + flag to the segment's part/partb/partc slot, no solve); 2 = split-K heavy-row
+// solve (slot = heavy row of a.desc: the reduced image of the row's first segment in place of
+// G + λI and the Gram).  The reference loops a heavy row inside one thread
+// (WALSEngine.cpp:277-287); SURVEY.md §5 "long rows".
+template <typename T, int NT, int MODE = 0>
 __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
   using C = BigCfg<T, NT>;
   using M = Mfma<T>;
@@ -390,9 +396,19 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const int64_t slot = a.row_begin + blockIdx.x;
-  const int64_t row = a.order ? a.order[slot] : slot;
-  const int64_t beg = a.rowptr[row];
-  const int64_t end = a.rowptr[row + 1];
+  int64_t row, beg, end, seg0 = 0;
+  if constexpr (MODE == 0) {
+    row = a.order ? a.order[slot] : slot;
+    beg = a.rowptr[row];
+    end = a.rowptr[row + 1];
+  } else {
+    const RowDesc d = a.desc[slot];
+    row = MODE == 2 ? (int64_t)d.row : -1;
+    seg0 = d.beg;                        // mode 2: the row's first segment slot
+    beg = MODE == 1 ? d.beg : 0;         // mode 1: the segment's signals
+    end = MODE == 1 ? d.beg + d.n : 0;   // mode 2: no signals
+  }
+  constexpr int NTT = C::NTT;
 
   // this wave's tiles (big_tile)
   int TI[TPW], TJ[TPW];
@@ -401,12 +417,22 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   acc_t acc[TPW];
 #pragma unroll
   for (int s = 0; s < TPW; ++s) {
+    if constexpr (MODE == 1) {
+      acc[s] = acc_t{0, 0, 0, 0};
+    } else if constexpr (MODE == 2) {
+      // the reduced image: [tile][lane][4] (the direct kernel's accumulator-image layout)
+      const T* img = a.part + seg0 * (NTT * 256);
+      const int t = TI[s] >= 0 ? tile_index(TI[s], TJ[s]) : 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 16 * TI[s] + M::crow(lane, r), j = 16 * TJ[s] + cl;
-      T g = TI[s] >= 0 ? a.G[(int64_t)i * KP + j] : T(0);
-      if (TI[s] >= 0 && i == j) g += (i < a.k) ? a.lambda : T(1);
-      acc[s][r] = g;
+      for (int r = 0; r < 4; ++r) acc[s][r] = TI[s] >= 0 ? img[(t * 64 + lane) * 4 + r] : T(0);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * TI[s] + M::crow(lane, r), j = 16 * TJ[s] + cl;
+        T g = TI[s] >= 0 ? a.G[(int64_t)i * KP + j] : T(0);
+        if (TI[s] >= 0 && i == j) g += (i < a.k) ? a.lambda : T(1);
+        acc[s][r] = g;
+      }
     }
   }
 
@@ -595,6 +621,31 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     }
   }
   }  // plain Gram
+  if constexpr (MODE == 1) {
+    // one segment of a heavy row: its partial tiles (image layout), rhs, Σc and flag
+    T* img = a.part + slot * (NTT * 256);
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      if (TI[s] >= 0) {
+        const int t = tile_index(TI[s], TJ[s]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) img[(t * 64 + lane) * 4 + r] = acc[s][r];
+      }
+    }
+    if (tid < KP) a.partb[slot * KP + tid] = bp;
+    if (tid == 0) {
+      a.partc[2 * slot] = cs;
+      a.partc[2 * slot + 1] = negw ? 1.0 : 0.0;
+    }
+    return;
+  }
+  if constexpr (MODE == 2) {
+    if (tid < KP) bp = a.partb[seg0 * KP + tid];
+    if (tid == 0) {
+      cs = a.partc[2 * seg0];
+      negw = a.partc[2 * seg0 + 1] != 0.0;
+    }
+  }
   if (tid < KP) {
     S.bw[tid] = bp;
     S.borig[tid] = bp;
@@ -820,13 +871,19 @@ __global__ __launch_bounds__(256) void gram_reduce_rt_kernel(const double* parti
   }
 }
 
+template <typename T, int NT, int MODE>
+static hipError_t launch_big_mode(const SolveArgs<T>& a, hipStream_t s) {
+  return launch_row_chunks(a, BigCfg<T, NT>::NTHR, [&](const SolveArgs<T>& c) {
+    hipLaunchKernelGGL((wals_big_kernel<T, NT, MODE>), dim3((unsigned)c.nrows),
+                       dim3(BigCfg<T, NT>::NTHR), 0, s, c);
+  });
+}
 template <typename T, int NT>
 static hipError_t launch_big_nt(const SolveArgs<T>& a, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
-  return launch_row_chunks(a, BigCfg<T, NT>::NTHR, [&](const SolveArgs<T>& c) {
-    hipLaunchKernelGGL((wals_big_kernel<T, NT>), dim3((unsigned)c.nrows),
-                       dim3(BigCfg<T, NT>::NTHR), 0, s, c);
-  });
+  if (a.seg_mode == 1) return launch_big_mode<T, NT, 1>(a, s);
+  if (a.seg_mode == 2) return launch_big_mode<T, NT, 2>(a, s);
+  return launch_big_mode<T, NT, 0>(a, s);
 }
 
 template <typename T, int NT>
@@ -836,6 +893,84 @@ static hipError_t launch_gram_tiles_nt(const T* Y, int64_t n, double* partial, i
     hipLaunchKernelGGL((gram_tiles_kernel<T, NT>), dim3(nblocks), dim3(BigCfg<T, NT>::NTHR), 0,
                        s, Y, n, rows_per_block, partial);
   return hipGetLastError();
+}
+
+// G + λI (padding diagonal 1) as the big kernel's tile image [tile][lane][4] (no column
+// permutation: the big kernel's tiles are canonical), for the split-K reduction
+template <typename T>
+__global__ void gimg_big_kernel(const T* G, int nt, int k, double lambda, T* img) {
+  using M = Mfma<T>;
+  const int KP = 16 * nt, NTT = nt * (nt + 1) / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NTT * 256) return;
+  const int r = idx & 3, lane = (idx >> 2) & 63, t = idx >> 8;
+  int I = 0;
+  while (tile_index(I + 1, 0) <= t) ++I;
+  const int J = t - tile_index(I, 0);
+  const int i = 16 * I + M::crow(lane, r), j = 16 * J + (lane & 15);
+  double g = (double)G[(int64_t)i * KP + j];
+  if (i == j) g += (i < k) ? lambda : 1.0;
+  img[idx] = (T)g;
+}
+
+// Split-K second pass for the big tilings (runtime tile count; heavy_reduce_kernel's contract,
+// wals_heavy.hip): one workgroup of 256 threads per (heavy row, tile) sums the row's segments
+// in segment order in fp64 with G + λI, rounds once and writes over the first segment's
+// slot; tile index NTT takes the rhs, Σc and the flag.
+template <typename T>
+__global__ __launch_bounds__(256) void heavy_reduce_big_kernel(T* part, T* partb, double* partc,
+                                                               const int64_t* hseg, int64_t h0,
+                                                               const T* Gimg, int nt) {
+  const int KP = 16 * nt, NTT = nt * (nt + 1) / 2;
+  const int t = blockIdx.y;
+  const int64_t h = h0 + blockIdx.x;
+  const int64_t s0 = hseg[h], s1 = hseg[h + 1];
+  const int tid = threadIdx.x;
+  if (t < NTT) {
+    const int64_t off = (int64_t)t * 256 + tid;
+    double v = (double)Gimg[off];
+    for (int64_t s = s0; s < s1; ++s) v += (double)part[s * ((int64_t)NTT * 256) + off];
+    part[s0 * ((int64_t)NTT * 256) + off] = (T)v;
+  } else {
+    for (int j = tid; j < KP; j += 256) {
+      double b = 0.0;
+      for (int64_t s = s0; s < s1; ++s) b += (double)partb[s * KP + j];
+      partb[s0 * KP + j] = (T)b;
+    }
+    if (tid == 0) {
+      double c = 0.0, f = 0.0;
+      for (int64_t s = s0; s < s1; ++s) {
+        c += partc[2 * s];
+        f = fmax(f, partc[2 * s + 1]);
+      }
+      partc[2 * s0] = c;
+      partc[2 * s0 + 1] = f;
+    }
+  }
+}
+
+template <typename T>
+static hipError_t heavy_reduce_big(T* part, T* partb, double* partc, const int64_t* hseg,
+                                   int64_t h0, int64_t nh, const T* G, T* Gimg, int nt, int k,
+                                   double lambda, hipStream_t s) {
+  const int NTT = nt * (nt + 1) / 2;
+  hipLaunchKernelGGL((gimg_big_kernel<T>), dim3(NTT), dim3(256), 0, s, G, nt, k, lambda, Gimg);
+  for (int64_t done = 0; done < nh; done += 65535) {
+    const int64_t cnt = nh - done < 65535 ? nh - done : 65535;
+    hipLaunchKernelGGL((heavy_reduce_big_kernel<T>), dim3((unsigned)cnt, NTT + 1), dim3(256), 0,
+                       s, part, partb, partc, hseg, h0 + done, (const T*)Gimg, nt);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_heavy_reduce_big(float* part, float* partb, double* partc, const int64_t* hseg,
+                                   int64_t h0, int64_t nh, const float* G, float* Gimg, int nt,
+                                   int k, double lambda, hipStream_t s) {
+  return heavy_reduce_big(part, partb, partc, hseg, h0, nh, G, Gimg, nt, k, lambda, s);
+}
+hipError_t launch_heavy_reduce_big(double* part, double* partb, double* partc, const int64_t* hseg,
+                                   int64_t h0, int64_t nh, const double* G, double* Gimg, int nt,
+                                   int k, double lambda, hipStream_t s) {
+  return heavy_reduce_big(part, partb, partc, hseg, h0, nh, G, Gimg, nt, k, lambda, s);
 }
 
 #define QMFX_BIG_SWITCH(NTV, CALL)        \

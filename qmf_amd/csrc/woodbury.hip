@@ -700,6 +700,32 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
       buf[I][0] = u[0], buf[I][1] = u[1], buf[I][2] = v[0], buf[I][3] = v[1];
     }
   };
+#if QMFX_EXP_XL2
+  // timing experiment (wrong results): the x' pass gathers from 1024 rows that stay in L2
+  const f64x2* zx[NTN];
+#pragma unroll
+  for (int I = 0; I < NTN; ++I) {
+    const int ce = __shfl(cr[I >> 2], (16 * I + cl) & 63, 64);
+    zx[I] = reinterpret_cast<const f64x2*>(a.Y + (uint64_t)((uint32_t)ce & 1023u) * KP);
+  }
+  auto load_chunk_x = [&](int s, double (&buf)[NTN][4]) {
+    const int c2 = 8 * s + 2 * kk;
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      const f64x2 u = zx[I][c2], v = zx[I][c2 + 1];
+      buf[I][0] = u[0], buf[I][1] = u[1], buf[I][2] = v[0], buf[I][3] = v[1];
+    }
+  };
+#elif QMFX_EXP_NOX
+  // timing experiment (wrong results): no x' gather at all
+  auto load_chunk_x = [&](int s, double (&buf)[NTN][4]) {
+#pragma unroll
+    for (int I = 0; I < NTN; ++I)
+      for (int c = 0; c < 4; ++c) buf[I][c] = (double)(s + I + c) * 1e-3;
+  };
+#else
+  auto load_chunk_x = load_chunk;
+#endif
 
   acc_t acc[NTT];
 #pragma unroll
@@ -771,7 +797,13 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
       if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
+#if QMFX_EXP_NOCHOL
+    // timing experiment (wrong results): no n×n factorization
+    if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
+    __syncthreads();
+#else
     chol_solve<double, NTN>(acc, S, lane, bad);
+#endif
     if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
     double xbl = 0.0;
 #pragma unroll
@@ -829,7 +861,13 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
       if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
     __syncthreads();
     if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
+#if QMFX_EXP_NOCHOL
+    // timing experiment (wrong results): no n×n factorization
+    if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
+    __syncthreads();
+#else
     chol_solve<double, NTN>(acc, S, lane, bad);
+#endif
     if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
@@ -849,11 +887,11 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     constexpr int XD = wb64_xdepth<NTN>();
     double buf[XD + 1][NTN][4];
 #pragma unroll
-    for (int s = 0; s < XD && s < NS; ++s) load_chunk(s, buf[s]);
+    for (int s = 0; s < XD && s < NS; ++s) load_chunk_x(s, buf[s]);
     double xbq = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s + XD < NS) load_chunk(s + XD, buf[(s + XD) % (XD + 1)]);
+      if (s + XD < NS) load_chunk_x(s + XD, buf[(s + XD) % (XD + 1)]);
       double (&cur)[NTN][4] = buf[s % (XD + 1)];
       double sx[4];
 #pragma unroll

@@ -78,6 +78,52 @@ def test_heavy_rows_match_oracle(k, precision, env, monkeypatch):
 
 
 @pytest.mark.parametrize("precision", [64, 32])
+def test_heavy_rows_k256_multiwave_match_oracle(precision):
+    """Split-K at k = 256 (the multi-wave k > 128 kernel used to solve a 10⁵-signal
+    row on one workgroup): the segment Grams, the fixed-order fp64 reduction and the solve
+    from the reduced image on wals_big_kernel, against the oracle: fp64 1e-9, fp32 1e-4 (or
+    the k·cond·u bound on the ill-conditioned item systems, as above)."""
+    u, i, v = heavy_dataset(105000, 300, 2, 100000, 1, seed=256 + precision)
+    o, c = make_pair(u, i, v, 256, precision, seed=9)
+    rc = c.row_classes(1)
+    assert rc["heavy"] == 2, rc
+    assert rc["segments"] >= 2 * (100000 // 8192), rc
+    for side in (0, 1):
+        if precision == 64:
+            tol = 1e-9
+        elif side == 0:
+            tol = 1e-4
+        else:
+            tol = max(1e-4, 256 * max_cond(o, 1) * 2.0 ** -24)
+        lo = o.iterate(side, NTHR)
+        ld = c.wals_half(side, ALPHA, LAM) / (o.nusers * o.nitems)
+        assert len(c.failed_rows()) == 0, side
+        assert rel_err(c.factors(side), o.factors(side)) < tol, side
+        assert abs(ld - lo) < tol * abs(lo), side
+        c.set_factors(side, o.factors(side))
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_heavy_split_k256_matches_whole_row_kernel(precision, monkeypatch):
+    """The k = 256 split-K route against the same rows solved whole by the multi-wave kernel
+    (QMFX_HEAVY_MIN=0), with short ragged segments."""
+    u, i, v = heavy_dataset(30000, 120, 2, 20000, 1, seed=4)
+    monkeypatch.setenv("QMFX_HEAVY_MIN", "0")
+    _, c0 = make_pair(u, i, v, 256, precision, seed=2)
+    assert c0.row_classes(1)["heavy"] == 0
+    monkeypatch.setenv("QMFX_HEAVY_MIN", "6000")
+    monkeypatch.setenv("QMFX_SEG_LEN", "2999")
+    _, c1 = make_pair(u, i, v, 256, precision, seed=2)
+    assert c1.row_classes(1)["heavy"] == 2
+    for side in (0, 1):
+        c0.wals_half(side, ALPHA, LAM)
+        c1.wals_half(side, ALPHA, LAM)
+        tol = 1e-11 if precision == 64 else 5e-4
+        assert rel_err(c1.factors(side), c0.factors(side)) < tol, side
+        c1.set_factors(side, c0.factors(side))
+
+
+@pytest.mark.parametrize("precision", [64, 32])
 def test_heavy_split_matches_whole_row_kernel(precision, monkeypatch):
     """The split-K route against the same rows solved whole by one wave
     (QMFX_HEAVY_MIN=0): equal to rounding (the segment order only regroups the sums)."""
