@@ -105,22 +105,33 @@ def test_heavy_rows_k256_multiwave_match_oracle(precision):
 
 @pytest.mark.parametrize("precision", [64, 32])
 def test_heavy_split_k256_matches_whole_row_kernel(precision, monkeypatch):
-    """The k = 256 split-K route against the same rows solved whole by the multi-wave kernel
-    (QMFX_HEAVY_MIN=0), with short ragged segments."""
+    """The k = 256 split-K route, with short ragged segments (partial LDS stages in every
+    segment), against the same rows solved whole by the multi-wave kernel
+    (QMFX_HEAVY_MIN=0), and both against the oracle."""
     u, i, v = heavy_dataset(30000, 120, 2, 20000, 1, seed=4)
     monkeypatch.setenv("QMFX_HEAVY_MIN", "0")
-    _, c0 = make_pair(u, i, v, 256, precision, seed=2)
+    o, c0 = make_pair(u, i, v, 256, precision, seed=2)
     assert c0.row_classes(1)["heavy"] == 0
     monkeypatch.setenv("QMFX_HEAVY_MIN", "6000")
     monkeypatch.setenv("QMFX_SEG_LEN", "2999")
     _, c1 = make_pair(u, i, v, 256, precision, seed=2)
     assert c1.row_classes(1)["heavy"] == 2
     for side in (0, 1):
+        o.iterate(side, NTHR)
         c0.wals_half(side, ALPHA, LAM)
         c1.wals_half(side, ALPHA, LAM)
-        tol = 1e-11 if precision == 64 else 5e-4
-        assert rel_err(c1.factors(side), c0.factors(side)) < tol, side
-        c1.set_factors(side, c0.factors(side))
+        x = o.factors(side)
+        # this data's item systems are ill-conditioned (users with one signal at k = 256:
+        # the user factors span ≤ 120 directions, λ = 0.05 holds the rest): both routes are
+        # held to the k·cond·u bound of their precision (the well-conditioned 10⁵-signal
+        # rows above are held to 1e-9 / 1e-4)
+        u_eps = 2.0 ** -53 if precision == 64 else 2.0 ** -24
+        base = 1e-9 if precision == 64 else 1e-4
+        tol = base if side == 0 else max(base, 256 * max_cond(o, 1) * u_eps)
+        e0, e1 = rel_err(c0.factors(side), x), rel_err(c1.factors(side), x)
+        assert e0 < tol and e1 < tol, (side, e0, e1)
+        c0.set_factors(side, x)
+        c1.set_factors(side, x)
 
 
 @pytest.mark.parametrize("precision", [64, 32])
