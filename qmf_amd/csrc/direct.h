@@ -12,6 +12,7 @@
 #include "kernels.h"
 #include "rowsolve.h"
 #include "chol.h"
+#include "chol4.h"
 #include "ntswitch.h"
 
 namespace qmfx {
@@ -748,7 +749,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
     }
     __syncthreads();
     if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
-    chol_solve<T, NT>(acc, S, lane, bad);
+    row_chol<T, NT>(acc, S, lane, bad);
     if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
 
     double xb = 0.0, xx = 0.0;

@@ -189,7 +189,8 @@ struct qmfx_ctx {
   int64_t trace_cap = 0;
   // per-class timing: 0 direct kernel, 1 whitened kernels (row solve + unwhiten), 2 whole half
   hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};
-  // solve pieces per half (QMFX_PIECES; default 1 on one rank, 4 with several) and their
+  // solve pieces per half (QMFX_PIECES; default 1 on one rank, 8 with several: the last
+  // piece's all-gather is the exposed part) and their
   // events: [piece][start, direct done, whitened done]; collectives run on comm_stream
   int npieces = 0;
   hipEvent_t evp[QMFX_MAX_PIECES][3] = {};
@@ -324,7 +325,7 @@ int max_whitened_ntn(const qmfx_ctx* c) {
 // direct bucket (heaviest rows first, for load balance), and uploads the order list.
 int npieces(const qmfx_ctx* c) {
   if (c->npieces > 0) return c->npieces;
-  return c->world > 1 ? 4 : 1;
+  return c->world > 1 ? 8 : 1;
 }
 
 // nnz-balanced split of rows [b, e) into p contiguous pieces → out[0..p]

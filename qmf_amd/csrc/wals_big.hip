@@ -49,7 +49,10 @@ struct BigCfg {
   static constexpr int KP = 16 * NT;
   static constexpr int NTT = NT * (NT + 1) / 2;
   // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave
-  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? 4 : 8);
+#ifndef QMFX_BIG_NW64_8
+#define QMFX_BIG_NW64_8 4  // waves per row at fp64 k ≤ 128 (only with QMFX_F64_BIG=1)
+#endif
+  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? QMFX_BIG_NW64_8 : 8);
   // split-bf16 Gram (fp32, NT = 2·NW): the loader threads split each staged element once
   // into bf16 hi/mid/lo planes ([column][signal], 32 signals = one 16x16x32 MFMA K step)
   // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
@@ -202,7 +205,7 @@ __device__ void big_panel_all(BigShared<T, NT>& S, int p, int wv, int lane, int&
   constexpr int KP = 16 * NT;
   constexpr int PLD = BigCfg<T, NT>::PLD;
   const int R = KP - 16 * p;
-  static_assert(48 * BigCfg<T, NT>::NW + 16 >= KP, "panel rows beyond the waves' lanes");
+  static_assert(48 * BigCfg<T, NT>::NW + 16 >= KP || !QMFX_BIG_PANEL_ALL, "panel rows beyond the waves' lanes");
   if (wv > 0 && 48 * wv + 16 >= R) return;  // no rows below the diagonal block for this wave
   const int q = lane < 16 ? lane : 48 * wv + lane;
   const bool live = q < R;
@@ -592,7 +595,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
         for (int k4 = 0; k4 < SIG; k4 += 4)
           big_gram_step<T, NT, W>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk]);
       };
-      static_assert(NW == 4 || NW == 8 || NW == 16, "wave count");
+      static_assert(NW == 2 || NW == 4 || NW == 8 || NW == 16, "wave count");
       if constexpr (C::REUSE) {
         dispatch_wave<NW>(wv, gram_stage);
       } else {

@@ -8,6 +8,7 @@
 #include <cstdlib>
 
 #include "chol.h"
+#include "chol4.h"
 #include "common.h"
 #include "kernels.h"
 #include "ntswitch.h"
@@ -624,6 +625,7 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 // whose register-resident Zₛ (half a row of doubles per lane) spilled.
 // ---------------------------------------------------------------------------------------
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+
 // chunks in flight ahead of the one being consumed: K pass (beside the NTT accumulator
 // tiles) and x' pass (after the solve, when the accumulators are dead)
 #ifndef QMFX_WB64_KD
@@ -802,7 +804,7 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
     __syncthreads();
 #else
-    chol_solve<double, NTN>(acc, S, lane, bad);
+    row_chol<double, NTN>(acc, S, lane, bad);
 #endif
     if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
     double xbl = 0.0;
@@ -866,7 +868,7 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
     __syncthreads();
 #else
-    chol_solve<double, NTN>(acc, S, lane, bad);
+    row_chol<double, NTN>(acc, S, lane, bad);
 #endif
     if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
 #pragma unroll
