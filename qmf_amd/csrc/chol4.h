@@ -205,11 +205,15 @@ __device__ __forceinline__ void chol4_solve(typename Mfma<T>::acc_t (&acc)[NT * 
   }
 }
 
-// The row kernels' factorization: fp64 systems of 32 rows and more on the 4-column panels
-// (QMFX_CHOL4=0 keeps chol_solve; one 16×16 tile stays on it: its panel staging would not fit
-// S.panel and it has no trailing tiles), fp32 on chol_solve.
+// The row kernels' factorization: chol_solve; QMFX_CHOL4=1 puts fp64 systems of 32 rows and
+// more on the 4-column panels (one 16×16 tile stays on chol_solve: its panel staging would
+// not fit S.panel).  Measured (profiles/r04/ab_chol4_c3_f64.txt, same box): SLOWER — C3 fp64
+// whitened class 187 → 198 ms, direct item half 188 → 210 ms; traces: the 64×64 factorization
+// 48K → 59K cycles, the 128×128 one 83K → 110K.  In one wave the rank-4 trailing MFMAs (70
+// instead of 40 at NT = 4, 444 instead of 336 at NT = 8) issue in order on the critical path,
+// and each 4-column panel pays two LDS round trips, where chol_solve pays one per 16 columns.
 #ifndef QMFX_CHOL4
-#define QMFX_CHOL4 1
+#define QMFX_CHOL4 0
 #endif
 template <typename T, int NT>
 __device__ __forceinline__ void row_chol(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],

@@ -15,6 +15,11 @@
 #include "chol4.h"
 #include "ntswitch.h"
 
+// timing experiments only (wrong results): the fp64 k > 64 Gram gathers rows col & MASK
+#ifndef QMFX_EXP_GRAM_MASK
+#define QMFX_EXP_GRAM_MASK 0xffffffffu
+#endif
+
 namespace qmfx {
 
 // (split3 / mma_split6: the fp32-accurate split-bf16 products, rowsolve.h; chol_solve: chol.h;
@@ -683,7 +688,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
         T v = __shfl(vr, kk, 64);
         T yn[NT];
         {
-          const T* yrow = a.Y + (uint64_t)(uint32_t)__shfl(cr, kk, 64) * KP + cl;
+          const T* yrow = a.Y + (uint64_t)((uint32_t)__shfl(cr, kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
 #pragma unroll
           for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
         }
@@ -699,7 +704,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
             // (lanes ≥ nst hold the zero row and v = 0)
             const int cn = __shfl(cr, jn < 64 ? jn : 63, 64);
             v = __shfl(vr, jn < 64 ? jn : 63, 64);
-            const T* yrow = a.Y + (uint64_t)(uint32_t)cn * KP + cl;
+            const T* yrow = a.Y + (uint64_t)((uint32_t)cn & QMFX_EXP_GRAM_MASK) * KP + cl;
 #pragma unroll
             for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
           }
