@@ -15,6 +15,10 @@
 #include "chol4.h"
 #include "ntswitch.h"
 
+// fp64 k > 64 Gram: two 4-signal steps per loop iteration (1) or one (0)
+#ifndef QMFX_F64_STEP2
+#define QMFX_F64_STEP2 0
+#endif
 // timing experiments only (wrong results): the fp64 k > 64 Gram gathers rows col & MASK
 #ifndef QMFX_EXP_GRAM_MASK
 #define QMFX_EXP_GRAM_MASK 0xffffffffu
@@ -680,6 +684,74 @@ void wals_direct_kernel(SolveArgs<T> a) {
       // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
       // so they contribute exactly nothing without per-value selects (only Σc needs the
       // validity)
+#if QMFX_F64_STEP2
+      // two 4-signal steps per iteration (signals 8s + kk and 8s + 4 + kk): the step
+      // boundary (the next rows' shuffle, its LDS round trip, the loads' issue, the moves of
+      // the landed rows) is paid once per 72 MFMAs instead of once per 36
+      for (int64_t base = beg; base < end; base += 64) {
+        const int nst = (int)(end - base < 64 ? end - base : 64);
+        const int cr = lane < nst ? a.col[base + lane] : a.zrow;
+        const T vr = lane < nst ? a.val[base + lane] : T(0);
+        bool validA = kk < nst, validB = 4 + kk < nst;
+        T vA = __shfl(vr, kk, 64), vB = __shfl(vr, 4 + kk, 64);
+        T ynA[NT], ynB[NT];
+        {
+          const T* ra = a.Y + (uint64_t)((uint32_t)__shfl(cr, kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
+          const T* rb = a.Y + (uint64_t)((uint32_t)__shfl(cr, 4 + kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
+#pragma unroll
+          for (int q = 0; q < NT; ++q) {
+            ynA[q] = ra[16 * q];
+            ynB[q] = rb[16 * q];
+          }
+        }
+        for (int s = 0; 8 * s < nst; ++s) {
+          T yA[NT], yB[NT];
+#pragma unroll
+          for (int q = 0; q < NT; ++q) {
+            yA[q] = ynA[q];
+            yB[q] = ynB[q];
+          }
+          const T wA = a.alpha * vA, wB = a.alpha * vB;
+          const T cwA = validA ? T(1) + wA : T(0), cwB = validB ? T(1) + wB : T(0);
+          const int jA = 8 * (s + 1) + kk, jB = jA + 4;
+          if (8 * (s + 1) < nst) {
+            // (lanes ≥ nst hold the zero row and v = 0)
+            const int cA = __shfl(cr, jA < 64 ? jA : 63, 64);
+            const int cB = __shfl(cr, jB < 64 ? jB : 63, 64);
+            vA = __shfl(vr, jA < 64 ? jA : 63, 64);
+            vB = __shfl(vr, jB < 64 ? jB : 63, 64);
+            const T* ra = a.Y + (uint64_t)((uint32_t)cA & QMFX_EXP_GRAM_MASK) * KP + cl;
+            const T* rb = a.Y + (uint64_t)((uint32_t)cB & QMFX_EXP_GRAM_MASK) * KP + cl;
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+              ynA[q] = ra[16 * q];
+              ynB[q] = rb[16 * q];
+            }
+          }
+          validA = jA < nst;
+          validB = jB < nst;
+#pragma unroll
+          for (int q = 0; q < NT; ++q) bpart[q] += cwA * yA[q] + cwB * yB[q];
+          csum += (double)cwA + (double)cwB;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+              const int t = tile_index(I, J);
+              acc[t] = M::mma(yA[I], wA * yA[J], acc[t]);
+            }
+          }
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+              const int t = tile_index(I, J);
+              acc[t] = M::mma(yB[I], wB * yB[J], acc[t]);
+            }
+          }
+        }
+      }
+#else
       for (int64_t base = beg; base < end; base += 64) {
         const int nst = (int)(end - base < 64 ? end - base : 64);
         const int cr = lane < nst ? a.col[base + lane] : a.zrow;
@@ -722,6 +794,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
           }
         }
       }
+#endif
     } else {
       gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
     }

@@ -17,6 +17,9 @@
 #include "common.h"
 #include "kernels.h"
 
+namespace qmfx {
+hipError_t launch_wals_direct2(const SolveArgs<double>& a, int nt, hipStream_t s);
+}
 using namespace qmfx;
 
 namespace {
@@ -516,6 +519,16 @@ FallbackArgs<T> fallback_args(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, i
   return a;
 }
 
+// fp64 k = 80..128 rows on two waves each (csrc/wals_direct2.hip; QMFX_DIRECT2=0: one wave)
+// fp64 k = 80..128 direct rows on two waves per row (wals_direct2.hip), QMFX_DIRECT2=1.  Off
+// by default: C3 fp64 item half 193.6 ms against the one-wave kernel's 189.0 (same box,
+// profiles/r04/ab_direct2_c3_f64.txt).
+bool use_direct2(const qmfx_ctx* c) {
+  if (c->prec != 64 || c->nt < 5 || c->nt > 8 || use_big_rows(c)) return false;
+  const char* e = std::getenv("QMFX_DIRECT2");
+  return e && std::atoi(e) != 0;
+}
+
 // One launch of the direct-row kernels over `n` slots from `b`: seg_mode 0 = slots of the
 // side's order (rows), 1 = split-K segments (d_seg), 2 = split-K heavy-row solves (d_heavy).
 template <typename T>
@@ -529,6 +542,9 @@ hipError_t launch_direct_t(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int6
   a.part = (T*)c->part;
   a.partb = (T*)c->partb;
   a.partc = c->partc;
+  if constexpr (sizeof(T) == 8) {
+    if (mode == 0 && use_direct2(c)) return launch_wals_direct2(a, c->nt, c->stream);
+  }
   return use_big_rows(c) ? launch_wals_big(a, c->nt, c->stream)
                          : launch_wals_direct(a, c->nt, c->stream);
 }

@@ -275,13 +275,16 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatc
         cd.set_factors(side, o.factors(side))
 
 
-@pytest.mark.parametrize("k,precision", [(144, 32), (192, 32), (256, 32), (80, 64), (128, 64),
-                                         (200, 64)])
-def test_large_k_multiwave_rows(k, precision):
+@pytest.mark.parametrize("k,precision,direct2", [(144, 32, 0), (192, 32, 0), (256, 32, 0),
+                                                 (80, 64, 0), (128, 64, 0), (200, 64, 0),
+                                                 (80, 64, 1), (112, 64, 1), (128, 64, 1)])
+def test_large_k_multiwave_rows(k, precision, direct2, monkeypatch):
     """k beyond one wave's registers (fp32 > 128, fp64 > 64): the multi-wave row kernel
     (LDS-staged Gram, distributed Cholesky) and the strip YᵀY, against the oracle at the
     reference's λ/α; rows from 1 to ~150 signals cover partial LDS stages and every
-    panel-slot count.  800 items ≫ k keeps the item systems well-posed for fp32."""
+    panel-slot count.  800 items ≫ k keeps the item systems well-posed for fp32.
+    direct2 = 1: fp64 direct rows on the two-wave kernel (QMFX_DIRECT2, wals_direct2.hip)."""
+    monkeypatch.setenv("QMFX_DIRECT2", str(direct2))
     u, i, v = synth(4000, 800, 100000, seed=k)
     o, c = make_pair(u, i, v, k, precision, seed=3)
     tol = 1e-9 if precision == 64 else 1e-4

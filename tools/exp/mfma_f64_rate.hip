@@ -5,8 +5,8 @@
 #include <cstdio>
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <int NACC, int NV>
-__global__ __launch_bounds__(64, 1) void bench(const double* in, double* out, long long* cyc, int iters) {
+template <int NACC, int NV, int WPS = 1>
+__global__ __launch_bounds__(64, WPS) void bench(const double* in, double* out, long long* cyc, int iters) {
   const int lane = threadIdx.x;
   double a = in[lane], b = in[lane + 64];
   f64x4 acc[NACC];
@@ -34,35 +34,35 @@ __global__ __launch_bounds__(64, 1) void bench(const double* in, double* out, lo
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int NACC, int NV>
+template <int NACC, int NV, int WPS = 1>
 void run(const double* din, double* dout, long long* dcyc) {
-  const int iters = 2000, blocks = 1024;
-  hipLaunchKernelGGL((bench<NACC, NV>), dim3(blocks), dim3(64), 0, 0, din, dout, dcyc, 10);
+  const int iters = 2000, blocks = 1024 * WPS;
+  hipLaunchKernelGGL((bench<NACC, NV, WPS>), dim3(blocks), dim3(64), 0, 0, din, dout, dcyc, 10);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  hipLaunchKernelGGL((bench<NACC, NV>), dim3(blocks), dim3(64), 0, 0, din, dout, dcyc, iters);
+  hipLaunchKernelGGL((bench<NACC, NV, WPS>), dim3(blocks), dim3(64), 0, 0, din, dout, dcyc, iters);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
-  long long c[blocks];
+  static long long c[4096];
   hipMemcpy(c, dcyc, sizeof(c), hipMemcpyDeviceToHost);
   double avg = 0;
   for (int i = 0; i < blocks; ++i) avg += (double)c[i];
   avg /= blocks;
   const double n = (double)iters * NACC;
-  printf("acc %2d valu/mfma %d: %.1f cyc/mfma (s_memtime), %.1f TF/s f64 MFMA (wall, %d waves)\n",
-         NACC, NV, avg / n, n * 2048.0 * blocks / (ms * 1e-3) / 1e12, blocks);
+  printf("acc %2d valu/mfma %d waves/SIMD %d: %.1f cyc/mfma per wave (s_memtime), %.1f TF/s f64 MFMA (wall, %d waves)\n",
+         NACC, NV, WPS, avg / n, n * 2048.0 * blocks / (ms * 1e-3) / 1e12, blocks);
 }
 
 int main() {
   double *din, *dout;
   long long* dcyc;
   hipMalloc(&din, 256 * sizeof(double));
-  hipMalloc(&dout, 1024 * 64 * sizeof(double));
-  hipMalloc(&dcyc, 1024 * sizeof(long long));
+  hipMalloc(&dout, 4096 * 64 * sizeof(double));
+  hipMalloc(&dcyc, 4096 * sizeof(long long));
   double h[256];
   for (int i = 0; i < 256; ++i) h[i] = 1.0 + 1e-3 * i;
   hipMemcpy(din, h, sizeof(h), hipMemcpyHostToDevice);
@@ -72,5 +72,10 @@ int main() {
   run<36, 2>(din, dout, dcyc);
   run<36, 4>(din, dout, dcyc);
   run<36, 8>(din, dout, dcyc);
+  run<18, 0, 2>(din, dout, dcyc);
+  run<18, 1, 2>(din, dout, dcyc);
+  run<18, 2, 2>(din, dout, dcyc);
+  run<10, 0, 2>(din, dout, dcyc);
+  run<10, 0, 4>(din, dout, dcyc);
   return 0;
 }

@@ -42,6 +42,12 @@ for lo, hi in bins:
           "  ".join(f"{nm} {v:7.0f}" for nm, v in zip(names, med)) + f"  total {med.sum():7.0f} cyc")
 # per-SIMD concurrency: key = (xcc, cu bits, simd)
 hw = t[:, 5]
+hw1 = (hw >> 40) & 0xffff  # two-wave kernels: wave 1's HW_ID
+if (hw1 != 0).any():
+    same_cu = ((hw >> 8) & 0xff) == ((hw1 >> 8) & 0xff)
+    same_simd = same_cu & (((hw >> 4) & 3) == ((hw1 >> 4) & 3))
+    print(f"two-wave rows: waves on the same CU {same_cu.mean():.3f}, on the same SIMD {same_simd.mean():.3f}")
+hw = hw & 0xffffffffff
 key = (hw >> 32) * 4096 + ((hw >> 8) & 0xff) * 4 + ((hw >> 4) & 3)
 order = np.lexsort((t[:, 0], key))
 t, key = t[order], key[order]
