@@ -32,14 +32,26 @@ struct CholLd {
   static constexpr int PLD = sizeof(T) == 4 ? 20 : 17;
 };
 
-template <typename T, int NT>
+// LTP = true keeps the diagonal L blocks (Lt) in the panel array instead of an array of their
+// own: panel p stages rows [0, 16·(NT−p)), so the rows past them are free, and block p goes
+// to rows [16·(NT−p−1), 16·(NT−p)) once panel p's last tile has been read back.  Half the LDS
+// (the whitened fp64 kernel at n ≤ 64: 19.5 → 10.8 KB per row, three rows per SIMD).
+template <typename T, int NT, bool LTP = false>
 struct CholShared {
   static constexpr int PLD = CholLd<T>::PLD;
+  static constexpr bool kLtInPanel = LTP;
   T panel[16 * NT * PLD];
-  T Lt[NT * 16 * PLD];
+  T Lt[LTP ? 1 : NT * 16 * PLD];
   T bw[16 * NT];
   T xs[16 * NT];
   T invd[16 * NT];
+  // row r of the transposed, column-scaled diagonal L blocks
+  __device__ __forceinline__ T* lt_row(int r) {
+    if constexpr (LTP)
+      return &panel[(16 * (NT - 1 - (r >> 4)) + (r & 15)) * PLD];
+    else
+      return &Lt[r * PLD];
+  }
 };
 
 // 16 consecutive values of an LDS row (b128 accesses for fp32)
@@ -82,13 +94,13 @@ __device__ __forceinline__ void csync() {
   }
 }
 
-template <typename T, int NT, bool WS = false>
+template <typename T, int NT, bool WS = false, bool LTP = false>
 __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
-                                           CholShared<T, NT>& S, int lane, int& bad) {
+                                           CholShared<T, NT, LTP>& S, int lane, int& bad) {
   using M = Mfma<T>;
   constexpr int KP = 16 * NT;
   constexpr int SLOTS = (KP + 63) / 64;
-  constexpr int PLD = CholShared<T, NT>::PLD;
+  constexpr int PLD = CholShared<T, NT, LTP>::PLD;
   const int cl = lane & 15;
   const int kk = lane >> 4;
 #pragma unroll
@@ -197,11 +209,19 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     csync<WS>();
     // diagonal block → Lt (transposed, scaled by the column's 1/L[q][q], zero on and above
     // the diagonal)
+    T ltv[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int idx = lane + 64 * it;
       const int r = idx >> 4, c = idx & 15;
-      S.Lt[(p * 16 + c) * PLD + r] = c < r ? S.panel[r * PLD + c] * S.invd[16 * p + c] : T(0);
+      ltv[it] = c < r ? S.panel[r * PLD + c] * S.invd[16 * p + c] : T(0);
+    }
+    if constexpr (!LTP) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = lane + 64 * it;
+        S.lt_row(p * 16 + (idx & 15))[idx >> 4] = ltv[it];
+      }
     }
     T fr[NT][4];
 #pragma unroll
@@ -215,6 +235,20 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         acc[t][r] = S.panel[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
+    }
+    if constexpr (LTP) {
+      // block p lands on the panel's last 16 rows (tile (NT−1, p), or at p = NT−1 the
+      // diagonal block itself): the reads of them above have returned first (the asm
+      // fence also keeps the compiler's order; one wave reads and writes these rows)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = lane + 64 * it;
+        S.lt_row(p * 16 + (idx & 15))[idx >> 4] = ltv[it];
+      }
+    }
+#pragma unroll
+    for (int I = p + 1; I < NT; ++I) {
 #pragma unroll
       for (int J = p + 1; J <= I; ++J) {
         const int tj = tile_index(I, J);
@@ -240,7 +274,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     part += shfl_xor(part, 32);
     T vm = (S.bw[16 * I + cl] - part) * S.invd[16 * I + cl];
     T lt[16];
-    lds_row_load(&S.Lt[(16 * I + cl) * PLD], lt);
+    lds_row_load(S.lt_row(16 * I + cl), lt);
 #pragma unroll
     for (int c = 15; c >= 0; --c) vm -= lt[c] * readlane(vm, c);
     if (lane < 16) S.xs[16 * I + lane] = vm;

@@ -215,10 +215,10 @@ __device__ __forceinline__ void chol4_solve(typename Mfma<T>::acc_t (&acc)[NT * 
 #ifndef QMFX_CHOL4
 #define QMFX_CHOL4 0
 #endif
-template <typename T, int NT>
+template <typename T, int NT, bool LTP>
 __device__ __forceinline__ void row_chol(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
-                                         CholShared<T, NT>& S, int lane, int& bad) {
-  if constexpr (sizeof(T) == 8 && NT >= 2 && QMFX_CHOL4)
+                                         CholShared<T, NT, LTP>& S, int lane, int& bad) {
+  if constexpr (sizeof(T) == 8 && NT >= 2 && QMFX_CHOL4 && !LTP)
     chol4_solve<T, NT>(acc, S, lane, bad);
   else
     chol_solve<T, NT>(acc, S, lane, bad);

@@ -634,22 +634,58 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 #ifndef QMFX_WB64_XD
 #define QMFX_WB64_XD 1
 #endif
+#ifndef QMFX_WB64_LTP
+#define QMFX_WB64_LTP 1
+#endif
+// waves per SIMD the streamed fp64 kernel is compiled for, by n×n tile count (n ≤ 16·NTN)
+#ifndef QMFX_WB64_WAVES
+#define QMFX_WB64_WAVES 2
+#endif
+#ifndef QMFX_WB64_WAVES3
+#define QMFX_WB64_WAVES3 2
+#endif
+#ifndef QMFX_WB64_WAVES2
+#define QMFX_WB64_WAVES2 2
+#endif
+template <int NTN>
+constexpr int wb64_waves() {
+  return NTN <= 2 ? QMFX_WB64_WAVES2 : NTN == 3 ? QMFX_WB64_WAVES3 : NTN == 4 ? QMFX_WB64_WAVES : 1;
+}
 template <int NTN>
 constexpr int wb64_kdepth() {
   return NTN <= 4 ? QMFX_WB64_KD : 1;
+}
+// 16-column chunks of Zₛ kept in registers from the K pass to the x' pass (the first KEEP;
+// the rest are gathered again): the registers the n×n Cholesky leaves free at two waves per
+// SIMD (fp64 whitened rows are bound by the fabric's random-row rate, so every chunk not
+// re-gathered is 1/NTK of the second pass's bytes)
+#ifndef QMFX_WB64_KEEP2
+#define QMFX_WB64_KEEP2 8
+#endif
+#ifndef QMFX_WB64_KEEP3
+#define QMFX_WB64_KEEP3 5
+#endif
+#ifndef QMFX_WB64_KEEP4
+#define QMFX_WB64_KEEP4 2
+#endif
+template <int NTK, int NTN>
+constexpr int wb64_keep() {
+  constexpr int k = NTN <= 2 ? QMFX_WB64_KEEP2 : NTN == 3 ? QMFX_WB64_KEEP3 : NTN == 4 ? QMFX_WB64_KEEP4 : 0;
+  return k < NTK ? k : NTK;
 }
 template <int NTN>
 constexpr int wb64_xdepth() {
   return NTN <= 4 ? QMFX_WB64_XD : 1;
 }
 template <int NTK, int NTN, bool TRACE = false>
-__global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
+__global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kernel(SolveArgs<double> a) {
   using M = Mfma<double>;
   using acc_t = typename M::acc_t;
   constexpr int KP = 16 * NTK;
   constexpr int NTT = NTN * (NTN + 1) / 2;
   constexpr int NS = NTK;  // 16-column chunks
-  __shared__ __attribute__((aligned(16))) CholShared<double, NTN> S;
+  // the diagonal L blocks ride in the panel array (chol.h, LTP): 10.8 KB per row at n ≤ 64
+  __shared__ __attribute__((aligned(16))) CholShared<double, NTN, QMFX_WB64_LTP != 0> S;
   __shared__ __attribute__((aligned(16))) double gq[16 * NTN];
 
   constexpr int H = NTN > 4 ? 2 : 1;  // signals per lane: e = lane + 64h
@@ -735,6 +771,8 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
   double sq[NTN];  // z_eᵀ Σ_{f∈Q} z_f over this lane's columns (rows with Q signals)
 #pragma unroll
   for (int I = 0; I < NTN; ++I) sq[I] = 0.0;
+  constexpr int KEEP = wb64_keep<NTK, NTN>();
+  double keep[KEEP > 0 ? KEEP : 1][NTN][4];
   {
     // a ring of KD + 1 chunk buffers: chunk s + KD is in flight while chunk s is consumed
     // (the loop unrolls fully, so every ring index is a compile-time constant)
@@ -746,6 +784,12 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     for (int s = 0; s < NS; ++s) {
       if (s + KD < NS) load_chunk(s + KD, buf[(s + KD) % (KD + 1)]);
       double (&cur)[NTN][4] = buf[s % (KD + 1)];
+      if (s < KEEP) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) keep[s < KEEP ? s : 0][I][c] = cur[I][c];
+      }
       if (hasQ) {
         double g[4];
 #pragma unroll
@@ -780,8 +824,13 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
 
   double xb = 0.0;
   double ul[NTN], cv[NTN];
+  // the n×n system: one factorization for both forms (a copy per form pushed the n = 64
+  // instance past three waves' registers)
+  double iw[H], rhs[H];
+  uint64_t mP[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) mP[h] = __ballot(isP[h]);
   if (!hasQ) {
-    double iw[H], rhs[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       iw[h] = isP[h] ? 1.0 / wl[h] : 1.0;
@@ -794,33 +843,9 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : 0.0;
     }
-#pragma unroll
-    for (int h = 0; h < H; ++h)
-      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
-    __syncthreads();
-    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
-#if QMFX_EXP_NOCHOL
-    // timing experiment (wrong results): no n×n factorization
-    if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
-    __syncthreads();
-#else
-    row_chol<double, NTN>(acc, S, lane, bad);
-#endif
-    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
-    double xbl = 0.0;
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const double ue = lane + 64 * h < 16 * NTN ? S.xs[lane + 64 * h] : 0.0;
-      xbl += isP[h] ? rhs[h] * (cwl[h] - ue) : 0.0;
-    }
-    xb = wave_sum(xbl);
-#pragma unroll
-    for (int I = 0; I < NTN; ++I) {
-      ul[I] = S.xs[16 * I + cl];
-      cv[I] = 0.0;
-    }
   } else {
-    double rhs[H], iw[H];
+    // Q signals (w = 0): u_Q = 1 moves to the right-hand side, the Q rows/columns become
+    // identity
 #pragma unroll
     for (int h = 0; h < H; ++h) rhs[h] = isP[h] ? cwl[h] / wl[h] : 0.0;
 #pragma unroll
@@ -831,13 +856,11 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
       if (kk == 0) gq[16 * I + cl] = v;
     }
     __syncthreads();
-    uint64_t mP[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const double kqv = lane + 64 * h < 16 * NTN ? gq[lane + 64 * h] : 0.0;
       if (isP[h]) rhs[h] -= kqv;
       iw[h] = isP[h] ? 1.0 / wl[h] : 0.0;
-      mP[h] = __ballot(isP[h]);
     }
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
@@ -858,19 +881,34 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
         }
       }
     }
+  }
 #pragma unroll
-    for (int h = 0; h < H; ++h)
-      if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
-    __syncthreads();
-    if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
+  for (int h = 0; h < H; ++h)
+    if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
+  __syncthreads();
+  if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
 #if QMFX_EXP_NOCHOL
-    // timing experiment (wrong results): no n×n factorization
-    if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
-    __syncthreads();
+  // timing experiment (wrong results): no n×n factorization
+  if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
+  __syncthreads();
 #else
-    row_chol<double, NTN>(acc, S, lane, bad);
+  row_chol<double, NTN>(acc, S, lane, bad);
 #endif
-    if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
+  if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
+  if (!hasQ) {
+    double xbl = 0.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const double ue = lane + 64 * h < 16 * NTN ? S.xs[lane + 64 * h] : 0.0;
+      xbl += isP[h] ? rhs[h] * (cwl[h] - ue) : 0.0;
+    }
+    xb = wave_sum(xbl);
+#pragma unroll
+    for (int I = 0; I < NTN; ++I) {
+      ul[I] = S.xs[16 * I + cl];
+      cv[I] = 0.0;
+    }
+  } else {
 #pragma unroll
     for (int I = 0; I < NTN; ++I) {
       const int e = 16 * I + cl;
@@ -887,14 +925,12 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
     // a deeper ring than the K pass (each chunk costs little compute: its loads would
     // otherwise be waited for one after the other)
     constexpr int XD = wb64_xdepth<NTN>();
+    constexpr int NG = NS - KEEP;  // chunks gathered again
     double buf[XD + 1][NTN][4];
 #pragma unroll
-    for (int s = 0; s < XD && s < NS; ++s) load_chunk_x(s, buf[s]);
+    for (int q = 0; q < XD && q < NG; ++q) load_chunk_x(KEEP + q, buf[q]);
     double xbq = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (s + XD < NS) load_chunk_x(s + XD, buf[(s + XD) % (XD + 1)]);
-      double (&cur)[NTN][4] = buf[s % (XD + 1)];
+    auto xchunk = [&](int s, const double (&cur)[NTN][4]) {
       double sx[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -924,6 +960,14 @@ __global__ __launch_bounds__(64, NTN <= 4 ? 2 : 1) void wals_woodbury_st64_kerne
         reinterpret_cast<f64x2*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
       }
       __builtin_amdgcn_sched_barrier(0);
+    };
+    // the kept chunks while the first gathers are in flight, then the gathered ring
+#pragma unroll
+    for (int s = 0; s < KEEP; ++s) xchunk(s, keep[s]);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      if (q + XD < NG) load_chunk_x(KEEP + q + XD, buf[(q + XD) % (XD + 1)]);
+      xchunk(KEEP + q, buf[q % (XD + 1)]);
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
   }
