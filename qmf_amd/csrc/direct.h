@@ -584,6 +584,9 @@ __device__ __forceinline__ void gram_f64_glds(const SolveArgs<double>& a, int64_
 // keep their accumulators in the whole (VGPR + AGPR) register file of one wave
 template <typename T, int NT>
 constexpr int direct_waves() {
+  // fp64 k = 48 / 64: 3 / 2 waves (asked for 4, the row solve settled there anyway and the
+  // split-K segment instance spilled 896 VGPRs)
+  if constexpr (sizeof(T) == 8 && NT >= 3 && NT <= 4) return NT == 3 ? 3 : 2;
   return Perm<NT>::template split<T> ? QMFX_WAVES_NT8 : (sizeof(T) == 8 && NT > 4 ? 1 : (NT <= 4 ? 4 : 2));
 }
 
