@@ -38,6 +38,12 @@
 #ifndef QMFX_BIG_PANEL_ALL
 #define QMFX_BIG_PANEL_ALL 1  // every wave factors the panel's diagonal block with its own rows
 #endif
+// fp64 k = 256 on the row-pair tile map (QMFX_BIG_PAIR64=1): half the Gram's LDS reads, but
+// 248 spilled VGPRs against 84 — C5 fp64 item half 1392 → 2175 ms (profiles/r04/
+// ab_big_pair64_c5_f64.txt).  Off by default.
+#ifndef QMFX_BIG_PAIR64
+#define QMFX_BIG_PAIR64 0
+#endif
 #ifndef QMFX_BIG_SPLIT
 #define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
 #endif
@@ -58,7 +64,11 @@ struct BigCfg {
   // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
   // planes once per stage for both rows
   static constexpr bool SPLIT = sizeof(T) == 4 && NT == 2 * NW && QMFX_BIG_SPLIT;
-  static constexpr int TPW = SPLIT ? NT + 1 : (NTT + NW - 1) / NW;
+  // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles) for the split Gram
+  // and for fp64 k = 256, whose Gram then reads each column block once per step for both
+  // rows (17 LDS reads per 17 MFMAs instead of 34 with the round-robin map)
+  static constexpr bool PAIR = SPLIT || (sizeof(T) == 8 && NT == 2 * NW && QMFX_BIG_PAIR64);
+  static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
   static constexpr int SIG = sizeof(T) == 4 ? QMFX_BIG_SIG32 : QMFX_BIG_SIG64;  // signals per LDS stage
@@ -74,7 +84,7 @@ struct BigCfg {
 // tile s of wave W: round-robin t = W + NW·s, or (split map) rows W and NT−1−W
 template <typename C>
 __host__ __device__ constexpr void big_tile(int W, int s, int& I, int& J) {
-  if constexpr (C::SPLIT) {
+  if constexpr (C::PAIR) {
     constexpr int NT = C::KP / 16;
     if (s <= W) {
       I = W;
@@ -598,6 +608,28 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       static_assert(NW == 2 || NW == 4 || NW == 8 || NW == 16, "wave count");
       if constexpr (C::REUSE) {
         dispatch_wave<NW>(wv, gram_stage);
+      } else if constexpr (C::PAIR) {
+        // rows A = W and B = NT−1−W: column block J's fragment serves tiles (B, J) and (A, J)
+        auto pair_stage = [&](auto wtag) __attribute__((always_inline)) {
+          constexpr int W = decltype(wtag)::value, A = W, B = NT - 1 - W;
+#pragma unroll 1
+          for (int k4 = 0; k4 < SIG; k4 += 4) {
+            const T* yk = sg + (k4 + kk) * KP + cl;
+            const T wk = S.w[buf][k4 + kk];
+            const T ya = yk[16 * A], yb = yk[16 * B];
+#pragma unroll
+            for (int J = 0; J <= B; ++J) {
+              const T yj = J == A ? ya : (J == B ? yb : yk[16 * J]);
+              const T wyj = wk * yj;
+              acc[W + 1 + J] = M::mma(yb, wyj, acc[W + 1 + J]);  // tile (B, J)
+              if (J <= A) acc[J] = M::mma(ya, wyj, acc[J]);     // tile (A, J)
+              // a few fragments in flight at a time (hoisting every load of the step
+              // spilled ~300 VGPRs beside the 136 accumulator registers)
+              if ((J & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        };
+        dispatch_wave<NW>(wv, pair_stage);
       } else {
 #pragma unroll 2
         for (int k4 = 0; k4 < SIG; k4 += 4) {

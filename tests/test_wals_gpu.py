@@ -276,7 +276,7 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatc
 
 
 @pytest.mark.parametrize("k,precision,direct2", [(144, 32, 0), (192, 32, 0), (256, 32, 0),
-                                                 (80, 64, 0), (128, 64, 0), (200, 64, 0),
+                                                 (80, 64, 0), (128, 64, 0), (200, 64, 0), (256, 64, 0),
                                                  (80, 64, 1), (112, 64, 1), (128, 64, 1)])
 def test_large_k_multiwave_rows(k, precision, direct2, monkeypatch):
     """k beyond one wave's registers (fp32 > 128, fp64 > 64): the multi-wave row kernel
