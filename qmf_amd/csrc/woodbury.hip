@@ -673,6 +673,23 @@ constexpr int wb64_keep() {
   constexpr int k = NTN <= 2 ? QMFX_WB64_KEEP2 : NTN == 3 ? QMFX_WB64_KEEP3 : NTN == 4 ? QMFX_WB64_KEEP4 : 0;
   return k < NTK ? k : NTK;
 }
+// and the next QMFX_WB64_KL{3,4,5} chunks kept in LDS (the room left under the per-CU LDS
+// at the kernel's waves per SIMD: ≤ 20 KB per row at n ≤ 64, ≤ 40 KB at n ≤ 80)
+#ifndef QMFX_WB64_KL3
+#define QMFX_WB64_KL3 1
+#endif
+#ifndef QMFX_WB64_KL4
+#define QMFX_WB64_KL4 1
+#endif
+#ifndef QMFX_WB64_KL5
+#define QMFX_WB64_KL5 2
+#endif
+template <int NTK, int NTN>
+constexpr int wb64_keep_lds() {
+  constexpr int k = NTN == 3 ? QMFX_WB64_KL3 : NTN == 4 ? QMFX_WB64_KL4 : NTN == 5 ? QMFX_WB64_KL5 : 0;
+  constexpr int room = NTK - wb64_keep<NTK, NTN>();
+  return k < room ? k : room;
+}
 template <int NTN>
 constexpr int wb64_xdepth() {
   return NTN <= 4 ? QMFX_WB64_XD : 1;
@@ -687,6 +704,9 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
   // the diagonal L blocks ride in the panel array (chol.h, LTP): 10.8 KB per row at n ≤ 64
   __shared__ __attribute__((aligned(16))) CholShared<double, NTN, QMFX_WB64_LTP != 0> S;
   __shared__ __attribute__((aligned(16))) double gq[16 * NTN];
+  // Zₛ chunks kept in LDS for the x' pass: [chunk][I·4 + c][lane]
+  constexpr int KL = wb64_keep_lds<NTK, NTN>();
+  __shared__ __attribute__((aligned(16))) double kl[KL > 0 ? KL : 1][NTN * 4][64];
 
   constexpr int H = NTN > 4 ? 2 : 1;  // signals per lane: e = lane + 64h
   const int lane = threadIdx.x;
@@ -789,6 +809,11 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
         for (int I = 0; I < NTN; ++I)
 #pragma unroll
           for (int c = 0; c < 4; ++c) keep[s < KEEP ? s : 0][I][c] = cur[I][c];
+      } else if (s < KEEP + KL) {
+#pragma unroll
+        for (int I = 0; I < NTN; ++I)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) kl[s - KEEP < KL ? s - KEEP : 0][4 * I + c][lane] = cur[I][c];
       }
       if (hasQ) {
         double g[4];
@@ -925,10 +950,11 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
     // a deeper ring than the K pass (each chunk costs little compute: its loads would
     // otherwise be waited for one after the other)
     constexpr int XD = wb64_xdepth<NTN>();
-    constexpr int NG = NS - KEEP;  // chunks gathered again
+    constexpr int KT = KEEP + KL;  // chunks kept on chip (registers, then LDS)
+    constexpr int NG = NS - KT;    // chunks gathered again
     double buf[XD + 1][NTN][4];
 #pragma unroll
-    for (int q = 0; q < XD && q < NG; ++q) load_chunk_x(KEEP + q, buf[q]);
+    for (int q = 0; q < XD && q < NG; ++q) load_chunk_x(KT + q, buf[q]);
     double xbq = 0.0;
     auto xchunk = [&](int s, const double (&cur)[NTN][4]) {
       double sx[4];
@@ -965,9 +991,18 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
 #pragma unroll
     for (int s = 0; s < KEEP; ++s) xchunk(s, keep[s]);
 #pragma unroll
+    for (int s = 0; s < KL; ++s) {
+      double cur[NTN][4];
+#pragma unroll
+      for (int I = 0; I < NTN; ++I)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cur[I][c] = kl[s][4 * I + c][lane];
+      xchunk(KEEP + s, cur);
+    }
+#pragma unroll
     for (int q = 0; q < NG; ++q) {
-      if (q + XD < NG) load_chunk_x(KEEP + q + XD, buf[(q + XD) % (XD + 1)]);
-      xchunk(KEEP + q, buf[q % (XD + 1)]);
+      if (q + XD < NG) load_chunk_x(KT + q + XD, buf[(q + XD) % (XD + 1)]);
+      xchunk(KT + q, buf[q % (XD + 1)]);
     }
     if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
   }
