@@ -637,6 +637,12 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 #ifndef QMFX_WB64_LTP
 #define QMFX_WB64_LTP 1
 #endif
+#ifndef QMFX_WB64_PRIO
+#define QMFX_WB64_PRIO 0  // s_setprio level of the n×n factorization (timing experiments)
+#endif
+#ifndef QMFX_WB64_PRIOK
+#define QMFX_WB64_PRIOK 0  // s_setprio level of the K pass (timing experiments)
+#endif
 // waves per SIMD the streamed fp64 kernel is compiled for, by n×n tile count (n ≤ 16·NTN)
 #ifndef QMFX_WB64_WAVES
 #define QMFX_WB64_WAVES 2
@@ -793,6 +799,7 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
   for (int I = 0; I < NTN; ++I) sq[I] = 0.0;
   constexpr int KEEP = wb64_keep<NTK, NTN>();
   double keep[KEEP > 0 ? KEEP : 1][NTN][4];
+  if constexpr (QMFX_WB64_PRIOK > 0) __builtin_amdgcn_s_setprio(QMFX_WB64_PRIOK);
   {
     // a ring of KD + 1 chunk buffers: chunk s + KD is in flight while chunk s is consumed
     // (the loop unrolls fully, so every ring index is a compile-time constant)
@@ -847,6 +854,7 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
     }
   }
 
+  if constexpr (QMFX_WB64_PRIOK > 0) __builtin_amdgcn_s_setprio(0);
   double xb = 0.0;
   double ul[NTN], cv[NTN];
   // the n×n system: one factorization for both forms (a copy per form pushed the n = 64
@@ -917,7 +925,10 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
   if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
   __syncthreads();
 #else
+  // the factorization's dependent chain first when another row shares the SIMD
+  if constexpr (QMFX_WB64_PRIO > 0) __builtin_amdgcn_s_setprio(QMFX_WB64_PRIO);
   row_chol<double, NTN>(acc, S, lane, bad);
+  if constexpr (QMFX_WB64_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 #endif
   if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
   if (!hasQ) {
