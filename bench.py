@@ -191,8 +191,9 @@ def cpu_epoch(ctx, cfg, nthreads):
                "t_build": round(t_build, 3), "loss": loss}
 
 
-def parity_check(ctx, cfg, nthreads, cfg_precision, nsample=1000):
-    """Full-size parity: one more (untimed) epoch; `nsample` rows of each half are re-solved
+def parity_check(ctx, cfg, nthreads, cfg_precision, nsample=1000, nheavy=16):
+    """Full-size parity: one more (untimed) epoch; `nsample` rows of each half (plus its
+    `nheavy` heaviest rows, reported apart) are re-solved
     by the oracle's updateFactorsForOne (WALSEngine.cpp:266-310) against the fixed side the
     device used (its own values), and compared with the device's rows and row losses."""
     po, _ = oracle_lib()
@@ -203,19 +204,28 @@ def parity_check(ctx, cfg, nthreads, cfg_precision, nsample=1000):
     U, lu = ctx.factors(0), ctx.row_losses(0)
     ctx.wals_half(1, ALPHA, LAM)
     I, li = ctx.factors(1), ctx.row_losses(1)
-    out = {"rows_per_half": nsample}
+    out = {"rows_per_half": nsample, "heaviest_rows_added": nheavy}
     worst = 0.0
     for side, Y, X, rl in ((0, I_prev, U, lu), (1, U, I, li)):
         rp, col, val = ctx.download_csr(side)
-        rows = np.sort(rng.choice(len(rp) - 1, nsample, replace=False))
+        nrow = len(rp) - 1
+        # uniform sample + the `nheavy` heaviest rows (on skewed data the split-K heavy rows are
+        # a few thousand of 1M: a uniform sample holds about 2 of them)
+        heavy = np.argsort(np.diff(rp), kind="stable")[-nheavy:]
+        uni = rng.choice(nrow, nsample, replace=False)
+        rows = np.union1d(uni, heavy)
         t0 = time.perf_counter()
         x, loss = po.solve_rows(Y, rp, col, val, rows, ALPHA, LAM, nthreads)
         dev = X[rows]
         row_err = np.linalg.norm(dev - x, axis=1) / np.maximum(np.linalg.norm(x, axis=1), 1e-300)
         rel = float(np.linalg.norm(dev - x) / np.linalg.norm(x))
         lrel = float(np.max(np.abs(rl[rows] - loss) / np.maximum(np.abs(loss), 1e-300)))
+        hv = np.isin(rows, heavy)
         out["side%d" % side] = {"max_row_rel_err": float(row_err.max()), "normwise_rel_err": rel,
                                 "max_row_loss_rel_err": lrel,
+                                "heavy_rows": int(hv.sum()),
+                                "heavy_min_signals": int(np.diff(rp)[heavy].min()),
+                                "heavy_max_row_rel_err": float(row_err[hv].max()),
                                 "oracle_s": round(time.perf_counter() - t0, 2)}
         worst = max(worst, float(row_err.max()))
         del rp, col, val
@@ -345,7 +355,11 @@ def bench_bpr(args, rank, world):
                              "bytes_per_launch": by},
                      "launch_ms": round(sec * 1e3, 3)},
         "eval_loss": loss,
+        "env": engine_env(os.environ),
     }
+    variant = qmf_amd._abi.build_variant()
+    if variant:
+        out["variant"] = variant
     traffic, tsrc = pmc_traffic(args.config, args.precision, "bpr_epoch_kernel", k)
     out["roofline"].update({"traffic": round(traffic, 0) if traffic else None,
                             "traffic_algorithmic_ratio": round(traffic / by, 3) if traffic else None,
@@ -466,6 +480,46 @@ def check_world(gpus, world, visible=None, local=0):
                          % (gpus, gpus, local, visible))
 
 
+# QMFX_* variables that make a run skip work (timing experiments): a line measured under one
+# is not a measurement of the product, so the bench refuses to print it
+WORK_SKIPPING_ENV = ("QMFX_ABLATE",)
+# variables of the harness itself (not engine knobs)
+_HARNESS_ENV = ("QMFX_BENCH_LIMIT_S",)
+
+
+def engine_env(environ):
+    """The QMFX_* engine knobs set in this run's environment (all are reported in the line)."""
+    return {k: v for k, v in sorted(environ.items())
+            if k.startswith("QMFX_") and k not in _HARNESS_ENV}
+
+
+def check_env(environ, variant, allow_variant=False):
+    """Raises SystemExit when the run would not measure the product: a work-skipping knob is
+    set, or the loaded library is a timing-variant build (qmfx_build_variant() != "") and
+    --allow-variant was not given."""
+    bad = [k for k in WORK_SKIPPING_ENV if environ.get(k, "0") not in ("", "0")]
+    if bad:
+        raise SystemExit("bench.py: %s set: the run would skip work; refusing to report a line"
+                         % ", ".join(bad))
+    if variant and not allow_variant:
+        raise SystemExit("bench.py: the loaded library is a timing-variant build (%s); "
+                         "pass --allow-variant to measure it anyway (the line is marked)" % variant)
+
+
+def exchange_fields(stats, steps, reduce_max):
+    """Per half (users, items) of a multi-rank run: the exchange on the collective stream and
+    the row solves, ms per half, each the max over ranks (reduce_max: list of floats -> the
+    elementwise max over ranks).  stats[side] = Context.exchange_stats(side) (sums over the
+    timed halves)."""
+    keys = ("exchange_ms", "exposed_ms", "solve_ms")
+    vals = [stats[side][k] / max(steps, 1) for side in (0, 1) for k in keys]
+    vals = reduce_max(vals)
+    out = {}
+    for side, name in ((0, "user_half"), (1, "item_half")):
+        out[name] = {k: round(vals[3 * side + i], 3) for i, k in enumerate(keys)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -477,6 +531,8 @@ def main():
     ap.add_argument("--cpu-baseline", default="epoch", choices=("sample", "epoch", "none"))
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--allow-variant", action="store_true",
+                    help="measure a timing-variant library (QMFX_LIB); the line is marked")
     args = ap.parse_args()
     if args.no_cpu_baseline:
         args.cpu_baseline = "none"
@@ -498,6 +554,8 @@ def main():
 
     import qmf_amd
 
+    variant = qmf_amd._abi.build_variant()
+    check_env(os.environ, variant, args.allow_variant)
     check_world(args.gpus, world, qmf_amd.device_count(), local)
     cpu_share()
     if args.config in BPR_CONFIGS:
@@ -570,6 +628,16 @@ def main():
                  # included: the fabric rate the class runs at)
                  "traffic_gbs": round(traffic / (d["launch_ms"] / 1e3) / 1e9, 1) if traffic else None,
                  "traffic_source": tsrc, "classes": classes})
+    xfields = None
+    if dist:
+        # the exchange per half, each field the max over ranks
+        def reduce_max(vals):
+            import torch
+            t = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return [float(v) for v in t]
+        xfields = exchange_fields({sd: ctx.exchange_stats(sd) for sd in (0, 1)}, args.steps,
+                                  reduce_max)
     half = ctx.kernel_stats(2)
     epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
     hbm_frac_epoch = epoch_bytes / (ms_epoch / 1e3) / (PEAK_HBM_GBS * 1e9)
@@ -597,7 +665,12 @@ def main():
         "roofline": roof,
         "hbm_roofline_frac_epoch": round(hbm_frac_epoch, 4),
         "loss": loss / nu / ni,
+        "env": engine_env(os.environ),
     }
+    if variant:
+        out["variant"] = variant
+    if xfields is not None:
+        out["exchange"] = xfields
     nthreads, host = cpu_share()
     if not args.no_parity and world == 1:
         t0 = time.perf_counter()

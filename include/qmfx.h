@@ -76,6 +76,11 @@ int qmfx_gen_synthetic(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t nn
  * is qmfx_gen_synthetic.  *nnz_out = unique pairs kept. */
 int qmfx_gen_synthetic_zipf(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64_t ndraws,
                             uint64_t seed, double zipf_s, int64_t* nnz_out);
+/* dst takes src's interactions (shape, id tables and both CSR orientations, copied device to
+ * device: over xGMI between GPUs) instead of building them again: one qmfx_group_signals for
+ * an n-GPU engine, then an import per peer before qmfx_dist_init_all shards them.  Both
+ * contexts must have the same precision; src must not be sharded. */
+int qmfx_import_signals(qmfx_ctx* dst, qmfx_ctx* src);
 /* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data).  values are
  * returned in double, exactly as the device holds them (an fp32 context's values widened). */
 int qmfx_download_csr(qmfx_ctx* ctx, int side, int64_t* rowptr, int32_t* colidx,
@@ -192,6 +197,20 @@ int qmfx_kernel_stats(qmfx_ctx* ctx, int cls, double* total_ms, int64_t* launche
 int qmfx_kernel_stats_side(qmfx_ctx* ctx, int cls, int side, double* total_ms, int64_t* launches,
                            double* flops, double* bytes);
 int qmfx_reset_stats(qmfx_ctx* ctx);
+/* Multi-rank halves (qmfx_dist_init with a communicator) that solved `side`, since reset:
+ * exchange_ms = Σ time of the per-piece broadcast groups on the collective stream (HIP events
+ * there; a piece's group starts when its solves are done and the previous group finished);
+ * exposed_ms = Σ from the last piece's solves done to its broadcasts done (the exchange not
+ * hidden behind solves); solve_ms = Σ row-solve time of the pieces.  Zero on one rank. */
+int qmfx_exchange_stats(qmfx_ctx* ctx, int side, double* exchange_ms, double* exposed_ms,
+                        double* solve_ms, int64_t* halves);
+/* The last qmfx_bpr_epoch's launch plan: concurrent waves (Hogwild width) and whether the user
+ * row's change was added atomically (1: a heavy user makes concurrent holders likely) or
+ * stored (0). */
+int qmfx_bpr_plan(qmfx_ctx* ctx, int* waves, int* atomic_user);
+/* "" for the product library; a timing-variant build (tools/build_variant.sh) returns its
+ * compile flags, so a variant loaded through QMFX_LIB is never taken for the product. */
+const char* qmfx_build_variant(void);
 
 /* ---- self tests ------------------------------------------------------------------------------ */
 /* C(16×16) = A(16×4)·B(4×16) through the kernels' MFMA operand/accumulator maps. */

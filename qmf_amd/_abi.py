@@ -38,6 +38,7 @@ SIGNATURES = {
     "qmfx_download_csr": [vp, c_int, P_i64, P_i32, P_f64],
     "qmfx_group_signals": [vp, vp, c_i64, P_i64, P_i64],
     "qmfx_get_ids": [vp, c_int, P_i64],
+    "qmfx_import_signals": [vp, vp],
     "qmfx_set_factors": [vp, c_int, P_f64],
     "qmfx_get_factors": [vp, c_int, P_f64],
     "qmfx_fill_uniform": [vp, c_int, c_dbl, c_u64],
@@ -65,9 +66,12 @@ SIGNATURES = {
     "qmfx_kernel_stats": [vp, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_kernel_stats_side": [vp, c_int, c_int, P_f64, P_i64, P_f64, P_f64],
     "qmfx_reset_stats": [vp],
+    "qmfx_exchange_stats": [vp, c_int, P_f64, P_f64, P_f64, P_i64],
+    "qmfx_bpr_plan": [vp, P_int, P_int],
+    "qmfx_build_variant": [],
     "qmfx_selftest_mfma": [c_int, c_int, P_f64, P_f64, P_f64],
 }
-_RESTYPE = {"qmfx_last_error": ctypes.c_char_p}
+_RESTYPE = {"qmfx_last_error": ctypes.c_char_p, "qmfx_build_variant": ctypes.c_char_p}
 
 _lib = None
 
@@ -107,6 +111,11 @@ def _p(a, t):
 
 def version():
     return lib().qmfx_version()
+
+
+def build_variant():
+    """'' for the product library; the compile flags of a timing-variant build."""
+    return lib().qmfx_build_variant().decode()
 
 
 def selftest_mfma(precision, A, B, device=0):
@@ -228,6 +237,11 @@ class Context:
                                         ctypes.byref(nu), ctypes.byref(ni)))
         self.nusers, self.nitems = nu.value, ni.value
         return self.ids(0), self.ids(1)
+
+    def import_signals(self, src):
+        """Take src's shape, ids and both CSRs device to device (qmfx_import_signals)."""
+        _check(lib().qmfx_import_signals(self.h, src.h))
+        self.nusers, self.nitems, _ = self.shape()
 
     def ids(self, side):
         out = np.empty(self.nusers if side == 0 else self.nitems, np.int64)
@@ -386,3 +400,17 @@ class Context:
 
     def reset_stats(self):
         _check(lib().qmfx_reset_stats(self.h))
+
+    def exchange_stats(self, side):
+        """Multi-rank halves that solved `side` since reset (include/qmfx.h
+        qmfx_exchange_stats): exchange_ms, exposed_ms, solve_ms (sums) and halves."""
+        x, t, sv, n = c_dbl(), c_dbl(), c_dbl(), c_i64()
+        _check(lib().qmfx_exchange_stats(self.h, side, ctypes.byref(x), ctypes.byref(t),
+                                         ctypes.byref(sv), ctypes.byref(n)))
+        return dict(exchange_ms=x.value, exposed_ms=t.value, solve_ms=sv.value, halves=n.value)
+
+    def bpr_plan(self):
+        """(waves, atomic_user) of the last bpr_epoch."""
+        w, a = c_int(), c_int()
+        _check(lib().qmfx_bpr_plan(self.h, ctypes.byref(w), ctypes.byref(a)))
+        return w.value, a.value

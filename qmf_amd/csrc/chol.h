@@ -20,9 +20,6 @@ namespace qmfx {
 // LDS transposed and column-scaled, Lt[q][c] = L[c][q]/L[q][q] (q < c, 0 elsewhere), so
 // the backward substitution is one readlane + one FMA per column.
 // ---------------------------------------------------------------------------------------
-#ifndef QMFX_CHOL_PK
-#define QMFX_CHOL_PK 1
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T>
@@ -32,23 +29,6 @@ struct CholLd {
   static constexpr int PLD = sizeof(T) == 4 ? 20 : 17;
 };
 
-// Panel columns with the diagonal block's column broadcast through LDS instead of readlanes:
-// every lane stores its column-c value and b (lanes 0..15's are the diagonal block's), every
-// lane reads entries c..15 and b_c back with broadcast reads (one address for the wave).  Column c+1 is updated first and stored before the
-// other columns' updates, so its LDS round trip overlaps them.  The readlane form spends
-// 2 v_readlane_b32 per broadcast value: 1344 of the 3952 instructions of the fp64 64×64
-// factorization.
-// Measured SLOWER (profiles/r04/ab_chol_ldsb_c3_f64.txt, same box): C3 fp64 whitened class
-// 179.6 → 181.8 ms, direct item half 188.7 → 190.0 ms, although the 64×64 factorization's
-// VALU instructions drop 3337 → 2166: the column chain is latency-bound, and the LDS round
-// trip is longer than the readlanes'.  Off by default.
-#ifndef QMFX_CHOL_LDSB
-#define QMFX_CHOL_LDSB 0
-#endif
-template <typename T>
-constexpr bool chol_ldsb() {
-  return QMFX_CHOL_LDSB && sizeof(T) == 8;
-}
 // LTP = true keeps the diagonal L blocks (Lt) in the panel array instead of an array of their
 // own: panel p stages rows [0, 16·(NT−p)), so the rows past them are free, and block p goes
 // to rows [16·(NT−p−1), 16·(NT−p)) once panel p's last tile has been read back.  Half the LDS
@@ -62,9 +42,6 @@ struct CholShared {
   T bw[16 * NT];
   T xs[16 * NT];
   T invd[16 * NT];
-  // QMFX_CHOL_LDSB (fp64): every lane's panel column c and b, double-buffered (lanes 0..15's
-  // entries are the diagonal block's column; unconditional stores, no exec-mask branches)
-  T bcast[chol_ldsb<T>() ? 2 : 1][chol_ldsb<T>() ? 128 : 1];
   // row r of the transposed, column-scaled diagonal L blocks
   __device__ __forceinline__ T* lt_row(int r) {
     if constexpr (LTP)
@@ -114,67 +91,6 @@ __device__ __forceinline__ void csync() {
   }
 }
 
-template <typename T, int NT, int SLOTS, bool LTP>
-__device__ __forceinline__ void chol_panel_ldsb(CholShared<T, NT, LTP>& S, T (&pa)[SLOTS][16],
-                                                T (&pb)[SLOTS], int R, int lane, T& invv, T& yv) {
-  S.bcast[0][lane] = pa[0][0];
-  S.bcast[0][64 + lane] = pb[0];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const int buf = c & 1;
-    T am[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m)
-      if (m >= c) am[m] = S.bcast[buf][m];
-    const T bc = S.bcast[buf][64 + c];
-    T ljj, inv;
-    pivot_sqrt(am[c], ljj, inv);
-    (void)ljj;
-    const bool me = lane == c;
-    invv = me ? inv : invv;
-    yv = me ? bc * inv : yv;
-    T lqs[SLOTS];
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      if (64 * s < R) {
-        const T lq = pa[s][c] * inv;
-        lqs[s] = lq * inv;
-        pa[s][c] = lq;
-        pb[s] -= lqs[s] * bc;
-      }
-    }
-    if (c < 15) {
-      // the next column first, and out to LDS while the rest of the update runs
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s)
-        if (64 * s < R) pa[s][c + 1 < 16 ? c + 1 : 15] -= lqs[s] * am[c + 1 < 16 ? c + 1 : 15];
-      S.bcast[buf ^ 1][lane] = pa[0][c + 1 < 16 ? c + 1 : 15];
-      S.bcast[buf ^ 1][64 + lane] = pb[0];
-    }
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      if (64 * s < R) {
-#pragma unroll
-        for (int m = 2; m < 16; ++m)
-          if (m > c + 1) pa[s][m] -= lqs[s] * am[m];
-      }
-    }
-    // one column per scheduling window: every row's updates are pinned here (left free, the
-    // compiler sinks each update to the column that reads it, keeping every column's
-    // broadcast and multiplier live: 250 VGPRs at 48×48)
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      if (64 * s < R) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (m >= c) asm volatile("" : "+v"(pa[s][m]));
-        asm volatile("" : "+v"(pb[s]));
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 template <typename T, int NT, bool WS = false, bool LTP = false>
 __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
                                            CholShared<T, NT, LTP>& S, int lane, int& bad) {
@@ -206,9 +122,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     }
     // lanes 0..15 collect the panel's 1/L[c][c] and y_c (lane c), stored once per panel
     T invv = T(0), yv = T(0);
-    if constexpr (chol_ldsb<T>()) {
-      chol_panel_ldsb<T, NT, SLOTS>(S, pa, pb, R, lane, invv, yv);
-    } else {
+    {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         // A[m][c] of the diagonal block's rows, broadcast before the pivot is known: the
@@ -237,7 +151,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
             const T lqs = lq * inv;
             pa[s][c] = lq;
             pb[s] -= lqs * bc;
-#if QMFX_CHOL_PK
             if constexpr (sizeof(T) == 4) {
               // packed pairs: one v_pk_fma_f32 per two columns (same rounding as two FMAs)
 #pragma unroll
@@ -252,9 +165,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
                   pa[s][m + 1] -= lqs * am[m + 1];
                 }
               }
-            } else
-#endif
-            {
+            } else {
 #pragma unroll
               for (int m = 1; m < 16; ++m)
                 if (m > c) pa[s][m] -= lqs * am[m];
@@ -363,6 +274,14 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     if (lane < 16) S.xs[16 * I + lane] = vm;
     csync<WS>();
   }
+}
+
+// The row kernels' factorization (the 4-column-panel form measured slower in round 4 is kept
+// under tools/exp/chol4.h)
+template <typename T, int NT, bool LTP>
+__device__ __forceinline__ void row_chol(typename Mfma<T>::acc_t (&acc)[NT * (NT + 1) / 2],
+                                         CholShared<T, NT, LTP>& S, int lane, int& bad) {
+  chol_solve<T, NT, false, LTP>(acc, S, lane, bad);
 }
 
 }  // namespace qmfx

@@ -12,17 +12,7 @@
 #include "kernels.h"
 #include "rowsolve.h"
 #include "chol.h"
-#include "chol4.h"
 #include "ntswitch.h"
-
-// fp64 k > 64 Gram: two 4-signal steps per loop iteration (1) or one (0)
-#ifndef QMFX_F64_STEP2
-#define QMFX_F64_STEP2 0
-#endif
-// timing experiments only (wrong results): the fp64 k > 64 Gram gathers rows col & MASK
-#ifndef QMFX_EXP_GRAM_MASK
-#define QMFX_EXP_GRAM_MASK 0xffffffffu
-#endif
 
 namespace qmfx {
 
@@ -110,13 +100,8 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   auto load_rows = [&](const int (&col)[8], vecW (&y)[8][NG]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-#ifdef QMFX_EXP_LOCAL_GATHER  // timing experiment: every gather hits a few cached rows
-      const vecW* yr =
-          reinterpret_cast<const vecW*>(a.Y + (uint64_t)(uint32_t)(col[j] & 63) * KP) + c;
-#else
       const vecW* yr =
           reinterpret_cast<const vecW*>(a.Y + (uint64_t)(uint32_t)col[j] * KP) + c;
-#endif
 #pragma unroll
       for (int G = 0; G < NG; ++G) y[j][G] = yr[16 * G];
     }
@@ -360,216 +345,6 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
 }
 
 // ---------------------------------------------------------------------------------------
-// fp64 direct Gram for KP a multiple of 32 (k = 96, 128): the gathered rows stream into an
-// LDS ring by LDS-DMA (global_load_lds_dwordx4: a load in flight holds no register), D steps
-// of 4 signals ahead, so ≈ D·4·KP·8 bytes per wave are in flight (28 KB at k = 128) instead
-// of one step's 4 KB: at one wave per SIMD the item half's gathers (≈4 TB/s of random 1-KB
-// rows) are latency-bound otherwise.  The row's (column, value) pairs arrive the same way,
-// 64-signal chunks two chunks ahead; the step loop runs whole chunks (past the row's end:
-// the fixed side's all-zero row with v = 0).  Every load is a glds, issued in a fixed
-// order, so the wait for step s is a compile-time vmcnt: the NI loads of each of the D − 1
-// steps issued after it, plus a chunk's NM metadata loads when one was issued in between.
-// The ring and the metadata live in the Cholesky's panel/Lt scratch (the Gram and the
-// factorization never overlap).
-// ---------------------------------------------------------------------------------------
-#ifndef QMFX_F64_RING
-#define QMFX_F64_RING 7
-#endif
-#ifndef QMFX_F64_GLDS
-#define QMFX_F64_GLDS 0
-#endif
-template <typename T, int NT>
-constexpr bool f64_glds() {
-  return QMFX_F64_GLDS && sizeof(T) == 8 && (NT == 6 || NT == 8);
-}
-// vmcnt-only s_waitcnt (the count must be an immediate)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-using glds_src_t = const __attribute__((address_space(1))) void*;
-using glds_dst_t = __attribute__((address_space(3))) void*;
-// LDS byte address of a __shared__ object
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-// LDS reads of LDS-DMA-written data as inline asm: the compiler cannot tell which LDS a DMA
-// wrote, so before any LDS read it can see it waits vmcnt(0) — draining the ring.  These
-// reads are invisible to it; the caller waits lgkmcnt itself (lds_wait) before the values
-// are used, passing them through the wait so no use is scheduled above it.
-template <int OFF>
-__device__ __forceinline__ double ds_read_f64(uint32_t addr) {
-  double v;
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
-  return v;
-}
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t ds_read_u32x4(uint32_t addr) {
-  u32x4_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-
-template <int NT, int D>
-__device__ __forceinline__ void gram_f64_glds(const SolveArgs<double>& a, int64_t beg, int n,
-                                              f64x4 (&acc)[NT * (NT + 1) / 2],
-                                              double (&bpart)[NT], double& csum, int lane,
-                                              double* ring, uint32_t* meta) {
-  constexpr int KP = 16 * NT;
-  constexpr int RB = 4 * KP * 8;  // bytes of one step's 4 rows
-  constexpr int NI = RB / 1024;   // glds_dwordx4 per step
-  constexpr int NM = 3;           // glds per metadata chunk: column, value low / high words
-  static_assert(RB % 1024 == 0 && D >= 2 && D <= 16, "ring geometry");
-  using M = Mfma<double>;
-  const int cl = lane & 15;
-  const int kk = lane >> 4;
-  if (n <= 0) return;
-  const int nch = (n + 63) >> 6;
-  const uint32_t zrow = (uint32_t)a.zrow;
-  // chunk c's (column, value) pairs → metadata slot c & 3 (positions past the row's end load
-  // its last signal again: in bounds, and replaced at use)
-  auto issue_meta = [&](int c) {
-    const int e = 64 * c + lane < n ? 64 * c + lane : n - 1;
-    const int64_t idx = beg + e;
-    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(meta + (c & 3) * 192));
-    const uint32_t* v32 = reinterpret_cast<const uint32_t*>(a.val + idx);
-    __builtin_amdgcn_global_load_lds((glds_src_t)(a.col + idx), (glds_dst_t)(uintptr_t)m, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((glds_src_t)v32, (glds_dst_t)(uintptr_t)(m + 256), 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((glds_src_t)(v32 + 1), (glds_dst_t)(uintptr_t)(m + 512), 4, 0,
-                                     0);
-  };
-  // step u's 4 column indices from the metadata (asm read; the caller waits lgkmcnt)
-  auto read_cols = [&](int u) {
-    const int e0 = 4 * u;
-    return ds_read_u32x4(lds_addr(meta + ((e0 >> 6) & 3) * 192 + (e0 & 63)));
-  };
-  // → wave-uniform columns (the zero row past the row's end)
-  auto uniform_cols = [&](int u, const u32x4_t& c4, uint32_t (&cs)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      cs[i] = 4 * u + i < n ? (uint32_t)__builtin_amdgcn_readfirstlane((int)c4[i]) : zrow;
-  };
-  // step u's 4 rows → ring slot `slot`; instruction i moves bytes 1024 i .. 1024 i + 1023 of
-  // the 4-row block
-  auto issue_rows = [&](const uint32_t (&cs)[4], int slot) {
-    double* dst = ring + slot * (4 * KP);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int b = 1024 * i + 16 * lane;
-      uint32_t col;
-      if constexpr (KP * 8 == 1024) {
-        col = cs[i];  // k = 128: instruction i is row i
-      } else {
-        const int r = b / (KP * 8);
-        col = r == 0 ? cs[0] : r == 1 ? cs[1] : r == 2 ? cs[2] : cs[3];
-      }
-      const double* src = a.Y + (uint64_t)col * KP + (b % (KP * 8)) / 8;
-      // the LDS destination must be wave-uniform (M0): readfirstlane keeps the compiler from
-      // wrapping the load in a waterfall loop over a VGPR-held address
-      const uint32_t da = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(dst + 128 * i));
-      __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)(uintptr_t)da, 16, 0, 0);
-    }
-  };
-  // step s's operands: lane (cl, kk) takes signal 4s + kk (its NT values, and the value's two
-  // words from metadata columns 64 + e and 128 + e)
-  auto read_step = [&](int s, int slot, double (&y)[NT], uint32_t& vlo, uint32_t& vhi) {
-    const uint32_t ya = lds_addr(ring + slot * (4 * KP) + kk * KP + cl);
-    [&]<int... Q>(std::integer_sequence<int, Q...>) {
-      ((y[Q] = ds_read_f64<128 * Q>(ya)), ...);
-    }(std::make_integer_sequence<int, NT>{});
-    const uint32_t ma = lds_addr(meta + ((s >> 4) & 3) * 192 + ((4 * s + kk) & 63));
-    asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(vlo) : "v"(ma));
-    asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(vhi) : "v"(ma));
-  };
-  // prologue: the first two chunks' metadata, then steps 0 .. D-2 (and chunk 2's metadata
-  // with step 0, as the loop does for every chunk's first step)
-  issue_meta(0);
-  issue_meta(1);
-  wait_vmcnt<0>();
-#pragma unroll
-  for (int u = 0; u < D - 1; ++u) {
-    u32x4_t c4 = read_cols(u);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4)::"memory");
-    uint32_t cs[4];
-    uniform_cols(u, c4, cs);
-    issue_rows(cs, u);
-    if (u % 16 == 0) issue_meta(u / 16 + 2);
-  }
-  // step 0's operands and step D-1's columns
-  wait_vmcnt<NI * (D - 2)>();
-  double y[NT];
-  uint32_t vlo, vhi;
-  read_step(0, 0, y, vlo, vhi);
-  u32x4_t c4 = read_cols(D - 1);
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4), "+v"(vlo), "+v"(vhi)::"memory");
-#pragma unroll
-  for (int q = 0; q < NT; ++q) asm volatile("" : "+v"(y[q]));
-  int slot_next = 1, slot_issue = D - 1;
-  const int S = 16 * nch;
-  // Iteration s: issue step s+D-1's rows (columns read one iteration earlier), wait for step
-  // s+1's rows, read step s+1's operands and step s+D's columns, THEN run step s's MFMAs
-  // with the operands read one iteration earlier, and wait for the reads only after them:
-  // the LDS latency hides behind the MFMAs instead of stalling each step twice.
-  for (int s = 0; s < S; ++s) {
-    {
-      uint32_t cs[4];
-      uniform_cols(s + D - 1, c4, cs);
-      issue_rows(cs, slot_issue);
-    }
-    if (((s + D - 1) & 15) == 0) issue_meta(((s + D - 1) >> 4) + 2);
-    slot_issue = slot_issue + 1 == D ? 0 : slot_issue + 1;
-    // loads issued after step s+1's: NI for each of steps s+2 .. s+D-1, plus a chunk's
-    // metadata when one of those opened a chunk (a metadata load issued with step s+1 itself
-    // is waited for too: conservative)
-    if (((s + 2 + 15) & ~15) <= s + D - 1)
-      wait_vmcnt<NI * (D - 2) + NM>();
-    else
-      wait_vmcnt<NI * (D - 2)>();
-    double yn[NT];
-    uint32_t vlon, vhin;
-    read_step(s + 1, slot_next, yn, vlon, vhin);
-    slot_next = slot_next + 1 == D ? 0 : slot_next + 1;
-    c4 = read_cols(s + D);
-    // the reads stay ahead of the MFMAs (the scheduler would otherwise sink them below)
-    __builtin_amdgcn_sched_barrier(0);
-    // step s
-    const int e = 4 * s + kk;
-    const double v =
-        e < n ? __builtin_bit_cast(double, (unsigned long long)vlo | ((unsigned long long)vhi << 32))
-              : 0.0;
-    const double w = a.alpha * v;
-    const double cw = e < n ? 1.0 + w : 0.0;
-    csum += cw;
-    double wy[NT];
-#pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      bpart[q] += cw * y[q];
-      wy[q] = w * y[q];
-    }
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-#pragma unroll
-      for (int J2 = 0; J2 <= I; ++J2) {
-        const int t = tile_index(I, J2);
-        acc[t] = M::mma(y[I], wy[J2], acc[t]);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // (and the wait stays behind them)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4), "+v"(vlon), "+v"(vhin)::"memory");
-#pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      asm volatile("" : "+v"(yn[q]));
-      y[q] = yn[q];
-    }
-    vlo = vlon;
-    vhi = vhin;
-  }
-  // the ring shares LDS with the Cholesky: every DMA (the dummy tail loads too) lands first
-  wait_vmcnt<0>();
-}
-
-// ---------------------------------------------------------------------------------------
 // Direct row kernel: one wave64 per row (slot order heaviest-first).  Gram
 // A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in registers, starting from
 // the tile image of G + λI (gimg_kernel: one coalesced 16-B load per tile and lane);
@@ -672,89 +447,12 @@ void wals_direct_kernel(SolveArgs<T> a) {
     }
     if constexpr (Perm<NT>::template split<T>) {
       gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
-    } else if constexpr (f64_glds<T, NT>()) {
-      // the ring and metadata inside the Cholesky's panel + Lt scratch
-      static_assert(sizeof(S.panel) + sizeof(S.Lt) >=
-                        (QMFX_F64_RING * 4 * KP + 4 * 192 / 2) * sizeof(double),
-                    "LDS ring does not fit the Cholesky scratch");
-      double* ring = reinterpret_cast<double*>(&S.panel[0]);
-      uint32_t* meta = reinterpret_cast<uint32_t*>(ring + QMFX_F64_RING * 4 * KP);
-      gram_f64_glds<NT, QMFX_F64_RING>(a, beg, (int)(end - beg), acc, bpart, csum, lane, ring,
-                                       meta);
     } else if constexpr (sizeof(T) == 8 && NT > 4) {
       // fp64 k > 64 (one wave, accumulators across the whole register file): the ring of
       // gram_plain costs more spills than its deeper prefetch gains; one step ahead
       // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
       // so they contribute exactly nothing without per-value selects (only Σc needs the
       // validity)
-#if QMFX_F64_STEP2
-      // two 4-signal steps per iteration (signals 8s + kk and 8s + 4 + kk): the step
-      // boundary (the next rows' shuffle, its LDS round trip, the loads' issue, the moves of
-      // the landed rows) is paid once per 72 MFMAs instead of once per 36
-      for (int64_t base = beg; base < end; base += 64) {
-        const int nst = (int)(end - base < 64 ? end - base : 64);
-        const int cr = lane < nst ? a.col[base + lane] : a.zrow;
-        const T vr = lane < nst ? a.val[base + lane] : T(0);
-        bool validA = kk < nst, validB = 4 + kk < nst;
-        T vA = __shfl(vr, kk, 64), vB = __shfl(vr, 4 + kk, 64);
-        T ynA[NT], ynB[NT];
-        {
-          const T* ra = a.Y + (uint64_t)((uint32_t)__shfl(cr, kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
-          const T* rb = a.Y + (uint64_t)((uint32_t)__shfl(cr, 4 + kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
-#pragma unroll
-          for (int q = 0; q < NT; ++q) {
-            ynA[q] = ra[16 * q];
-            ynB[q] = rb[16 * q];
-          }
-        }
-        for (int s = 0; 8 * s < nst; ++s) {
-          T yA[NT], yB[NT];
-#pragma unroll
-          for (int q = 0; q < NT; ++q) {
-            yA[q] = ynA[q];
-            yB[q] = ynB[q];
-          }
-          const T wA = a.alpha * vA, wB = a.alpha * vB;
-          const T cwA = validA ? T(1) + wA : T(0), cwB = validB ? T(1) + wB : T(0);
-          const int jA = 8 * (s + 1) + kk, jB = jA + 4;
-          if (8 * (s + 1) < nst) {
-            // (lanes ≥ nst hold the zero row and v = 0)
-            const int cA = __shfl(cr, jA < 64 ? jA : 63, 64);
-            const int cB = __shfl(cr, jB < 64 ? jB : 63, 64);
-            vA = __shfl(vr, jA < 64 ? jA : 63, 64);
-            vB = __shfl(vr, jB < 64 ? jB : 63, 64);
-            const T* ra = a.Y + (uint64_t)((uint32_t)cA & QMFX_EXP_GRAM_MASK) * KP + cl;
-            const T* rb = a.Y + (uint64_t)((uint32_t)cB & QMFX_EXP_GRAM_MASK) * KP + cl;
-#pragma unroll
-            for (int q = 0; q < NT; ++q) {
-              ynA[q] = ra[16 * q];
-              ynB[q] = rb[16 * q];
-            }
-          }
-          validA = jA < nst;
-          validB = jB < nst;
-#pragma unroll
-          for (int q = 0; q < NT; ++q) bpart[q] += cwA * yA[q] + cwB * yB[q];
-          csum += (double)cwA + (double)cwB;
-#pragma unroll
-          for (int I = 0; I < NT; ++I) {
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-              const int t = tile_index(I, J);
-              acc[t] = M::mma(yA[I], wA * yA[J], acc[t]);
-            }
-          }
-#pragma unroll
-          for (int I = 0; I < NT; ++I) {
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-              const int t = tile_index(I, J);
-              acc[t] = M::mma(yB[I], wB * yB[J], acc[t]);
-            }
-          }
-        }
-      }
-#else
       for (int64_t base = beg; base < end; base += 64) {
         const int nst = (int)(end - base < 64 ? end - base : 64);
         const int cr = lane < nst ? a.col[base + lane] : a.zrow;
@@ -763,7 +461,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
         T v = __shfl(vr, kk, 64);
         T yn[NT];
         {
-          const T* yrow = a.Y + (uint64_t)((uint32_t)__shfl(cr, kk, 64) & QMFX_EXP_GRAM_MASK) * KP + cl;
+          const T* yrow = a.Y + (uint64_t)(uint32_t)__shfl(cr, kk, 64) * KP + cl;
 #pragma unroll
           for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
         }
@@ -779,7 +477,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
             // (lanes ≥ nst hold the zero row and v = 0)
             const int cn = __shfl(cr, jn < 64 ? jn : 63, 64);
             v = __shfl(vr, jn < 64 ? jn : 63, 64);
-            const T* yrow = a.Y + (uint64_t)((uint32_t)cn & QMFX_EXP_GRAM_MASK) * KP + cl;
+            const T* yrow = a.Y + (uint64_t)(uint32_t)cn * KP + cl;
 #pragma unroll
             for (int q = 0; q < NT; ++q) yn[q] = yrow[16 * q];
           }
@@ -797,7 +495,6 @@ void wals_direct_kernel(SolveArgs<T> a) {
           }
         }
       }
-#endif
     } else {
       gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
     }

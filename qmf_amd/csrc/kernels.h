@@ -31,8 +31,6 @@ struct SolveArgs {
   T alpha;
   T lambda;
   int k;                  // real number of factors (≤ KP)
-  int ablate;             // timing experiments only: bit0 skip Gram loop, bit1 skip panel
-                          // factorization, bit2 skip trailing MFMA update, bit3 skip backward
   const RowDesc* desc;    // per-slot descriptors (persistent row kernels; indexed like order)
   const T* Gimg;          // direct kernel: G + λI as per-lane accumulator tiles (gimg_kernel)
   uint64_t* trace;        // diagnostics only (QMFX_TRACE): per-slot phase timestamps
@@ -102,28 +100,8 @@ hipError_t launch_gram_big(const double* Y, int64_t n, int nt, double* G, double
                            int max_blocks, hipStream_t s);
 // whitened-row buckets: n ≤ 16·NTN, NTN = 1..kMaxNTN (NTN > 4 only for fp32 k = 256)
 constexpr int kMaxNTN = 8;
-// Whitened-kernel routes (timing comparisons; the defaults are the measured best).  Read
-// from the environment ONCE per context, at qmfx_create, so the buckets a context builds
-// and the kernels it launches for them always agree.
-struct KernelSel {
-  bool wb_stream = true;  // QMFX_WB_STREAM=0: fp32 register-resident whitened kernel
-  bool wb_st64 = true;    // QMFX_WB_ST64=0: fp64 k = 80..128 multi-wave whitened kernel
-  bool wb_mw = false;     // QMFX_WB_MW=1: fp32 k = 256 multi-wave whitened kernel
-  int mw_f64_ntn4 = 2;    // QMFX_MW_F64_NTN4: waves per row of that kernel's n ≤ 64 bucket
-  int k128_ntn = 8;       // QMFX_WB_K128_NTN: largest fp32 k = 128 bucket
-  int f64_ntn = 5;        // QMFX_WB_F64_NTN: largest fp64 k = 128 bucket
-  int k256_ntn = 8;       // QMFX_WB_K256_NTN: largest fp32 k = 256 bucket
-};
-KernelSel read_kernel_sel();
-// largest whitened bucket at fp32 k = 256: 8 on the streamed kernel, 4 on the multi-wave
-// (QMFX_WB_MW=1) or register-resident (QMFX_WB_STREAM=0) ones
-int whitened_max_ntn_k256(const KernelSel& ks);
-int whitened_max_ntn_k128(const KernelSel& ks);
-int whitened_max_ntn_f64_k128(const KernelSel& ks);
-hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, const KernelSel& ks,
-                                hipStream_t s);
-hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn,
-                                const KernelSel& ks, hipStream_t s);
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s);
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s);
 hipError_t launch_whiten(const float* in, float* out, const int64_t* order, int64_t nrows,
                          int nt, const float* Linv, double* rowloss, double lambda,
                          bool unwhiten, hipStream_t s);

@@ -17,9 +17,6 @@
 #include "common.h"
 #include "kernels.h"
 
-namespace qmfx {
-hipError_t launch_wals_direct2(const SolveArgs<double>& a, int nt, hipStream_t s);
-}
 using namespace qmfx;
 
 namespace {
@@ -161,9 +158,10 @@ struct qmfx_ctx {
   double* ev_sq = nullptr;
   double* ev_udbl = nullptr;
   uint64_t bpr_epochs = 0;
-  int ablate = 0;  // QMFX_ABLATE (timing experiments only)
+  // QMFX_FAULT_COMM_RANK (tests): the rank whose next piece broadcast fails as if RCCL had
+  // failed, read once at create (-1: none)
+  int fault_comm_rank = -1;
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
-  KernelSel ksel;  // whitened-kernel routes, read once at create
   // the half-epoch in progress (qmfx_wals_half's phases)
   struct HalfStateT {
     int side = 0;
@@ -199,6 +197,15 @@ struct qmfx_ctx {
   hipEvent_t evp[QMFX_MAX_PIECES][3] = {};
   hipEvent_t ev_sum = nullptr, ev_comm = nullptr;
   hipStream_t comm_stream = nullptr;
+  // multi-rank halves: per piece, the collective stream's [start, end] of its broadcasts
+  // (start = when the stream reached them: the piece's solves done and the previous piece's
+  // broadcasts finished); per solved side since reset: Σ broadcast time, the exposed tail
+  // (last piece's solves done → its broadcasts done) and Σ solve time of the pieces
+  hipEvent_t evx[QMFX_MAX_PIECES][2] = {};
+  double xch_ms[2] = {0, 0}, xch_tail_ms[2] = {0, 0}, xch_solve_ms[2] = {0, 0};
+  int64_t xch_halves[2] = {0, 0};
+  // BPR launch plan of the last epoch (qmfx_bpr_plan)
+  int bpr_waves = 0, bpr_atomic_user = 0;
   double cls_ms[3] = {0, 0, 0}, cls_flops[3] = {0, 0, 0}, cls_bytes[3] = {0, 0, 0};
   int64_t cls_launches[3] = {0, 0, 0};
   // the same per solved side (a class's launches differ by side: at C3 the direct kernel
@@ -291,37 +298,24 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 // row kernel and the tiled YᵀY (wals_big.hip).
 // YᵀY on the tiled multi-wave kernel (fp32 k > 128, fp64 k > 64)
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
-// direct rows on the multi-wave row kernel: k > 128.  fp64 k = 80..128 runs the one-wave
-// direct kernel with its accumulators across the VGPR + AGPR file (QMFX_F64_BIG=1 keeps the
-// multi-wave kernel there, for comparisons).
-bool use_big_rows(const qmfx_ctx* c) {
-  if (c->nt > 8) return true;
-  // fp32 k ≤ 128: the one-wave direct kernel (measured at C3's item half: 76 ms direct vs
-  // 153 ms on the 4-wave split-bf16 multi-wave kernel)
-  if (c->prec == 32) return false;
-  if (c->nt <= 4) return false;
-  const char* e = std::getenv("QMFX_F64_BIG");
-  return e && std::atoi(e) != 0;
-}
+// direct rows on the multi-wave row kernel: k > 128 (fp64 k = 80..128 runs the one-wave
+// direct kernel with its accumulators across the VGPR + AGPR file)
+bool use_big_rows(const qmfx_ctx* c) { return c->nt > 8; }
 
+// Largest whitened-row bucket (NTN: n ≤ 16·NTN) for this factor tiling: n ≤ KP/2
+// and ≤ 64, except on the streamed kernels' two-signals-per-lane buckets: fp32 k = 128 / 256
+// up to n = 128, fp64 k = 128 / 256 up to n = 80 (n = 81..96 spilled 64 VGPRs; those rows stay
+// direct).
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
-  // multi-wave tilings: the whitened kernels exist for fp32 k = 256 (NT = 16) and fp64
-  // k = 80..128 and 256 (NT = 5..8 and 16: the streamed fp64 kernel)
-  if (use_big(c)) {
-    // fp32 k = 256: the streamed kernel takes n ≤ 128 (two signals per lane past 64), the
-    // multi-wave one (QMFX_WB_MW=1) n ≤ 64
-    if (c->prec == 32) return c->nt == 16 ? whitened_max_ntn_k256(c->ksel) : 0;
-    if (c->nt == 8) return whitened_max_ntn_f64_k128(c->ksel);
-    // fp64 k = 256: the streamed fp64 kernel (n ≤ 80), or every row on the big kernel
-    if (c->nt == 16) return c->ksel.wb_st64 ? whitened_max_ntn_f64_k128(c->ksel) : 0;
-    return c->nt <= 8 ? std::min(c->nt / 2, 4) : 0;
+  if (c->prec == 32) {
+    if (c->nt == 8 || c->nt == 16) return 8;
+    if (c->nt > 8) return 0;  // fp32 k = 144..240: every row on the big k×k kernel
+    return std::min(c->nt / 2, 4);
   }
-  int m = c->nt / 2;
-  if (m > 4) m = 4;
-  if (c->prec == 64 && m > 2) m = 2;
-  if (c->prec == 32 && c->nt == 8) m = whitened_max_ntn_k128(c->ksel);
-  return m;
+  if (c->nt == 8 || c->nt == 16) return 5;
+  if (c->nt > 8) return 0;
+  return std::min(c->nt / 2, c->nt <= 4 ? 2 : 4);
 }
 
 // Splits this rank's rows of `side` into whitened buckets (by padded signal count) and the
@@ -519,32 +513,19 @@ FallbackArgs<T> fallback_args(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, i
   return a;
 }
 
-// fp64 k = 80..128 rows on two waves each (csrc/wals_direct2.hip; QMFX_DIRECT2=0: one wave)
-// fp64 k = 80..128 direct rows on two waves per row (wals_direct2.hip), QMFX_DIRECT2=1.  Off
-// by default: C3 fp64 item half 193.6 ms against the one-wave kernel's 189.0 (same box,
-// profiles/r04/ab_direct2_c3_f64.txt).
-bool use_direct2(const qmfx_ctx* c) {
-  if (c->prec != 64 || c->nt < 5 || c->nt > 8 || use_big_rows(c)) return false;
-  const char* e = std::getenv("QMFX_DIRECT2");
-  return e && std::atoi(e) != 0;
-}
-
 // One launch of the direct-row kernels over `n` slots from `b`: seg_mode 0 = slots of the
 // side's order (rows), 1 = split-K segments (d_seg), 2 = split-K heavy-row solves (d_heavy).
 template <typename T>
 hipError_t launch_direct_t(qmfx_ctx* c, const SideBuf& L, const SideBuf& R, int64_t b, int64_t n,
                            double alpha, double lambda, const char* trace_path, int mode) {
   SolveArgs<T> a{L.rowptr, colp(L), valp<T>(L), (const T*)R.F, (const T*)c->G, (T*)L.F,
-                 c->rowloss, c->status, L.d_order, b, n, (T)alpha, (T)lambda, c->k, c->ablate,
+                 c->rowloss, c->status, L.d_order, b, n, (T)alpha, (T)lambda, c->k,
                  mode == 1 ? L.d_seg : mode == 2 ? L.d_heavy : L.d_desc, (const T*)c->Gimg,
                  (trace_path && mode == 0) ? c->trace : nullptr, (int32_t)R.n};
   a.seg_mode = mode;
   a.part = (T*)c->part;
   a.partb = (T*)c->partb;
   a.partc = c->partc;
-  if constexpr (sizeof(T) == 8) {
-    if (mode == 0 && use_direct2(c)) return launch_wals_direct2(a, c->nt, c->stream);
-  }
   return use_big_rows(c) ? launch_wals_big(a, c->nt, c->stream)
                          : launch_wals_direct(a, c->nt, c->stream);
 }
@@ -585,9 +566,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->nt = nt;
   c->kp = 16 * nt;
   c->esz = precision == 32 ? 4 : 8;
-  if (const char* ab = std::getenv("QMFX_ABLATE")) c->ablate = std::atoi(ab);
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
-  c->ksel = read_kernel_sel();
+  if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK")) c->fault_comm_rank = std::atoi(f);
   if (const char* hm = std::getenv("QMFX_HEAVY_MIN")) c->heavy_min = std::max<int64_t>(std::atoll(hm), 0);
   if (const char* sl = std::getenv("QMFX_SEG_LEN"))
     c->seg_len = std::min<int64_t>(std::max<int64_t>(std::atoll(sl), 64), INT32_MAX);
@@ -608,6 +588,8 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->evh[i]);
   for (int i = 0; i < QMFX_MAX_PIECES && e == hipSuccess; ++i)
     for (int j = 0; j < 3 && e == hipSuccess; ++j) e = hipEventCreate(&c->evp[i][j]);
+  for (int i = 0; i < QMFX_MAX_PIECES && e == hipSuccess; ++i)
+    for (int j = 0; j < 2 && e == hipSuccess; ++j) e = hipEventCreate(&c->evx[i][j]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_sum, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&c->Linv, (size_t)c->kp * c->kp * c->esz);
@@ -635,6 +617,9 @@ int qmfx_destroy(qmfx_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   for (auto& row : c->evp)
+    for (auto& ev : row)
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto& row : c->evx)
     for (auto& ev : row)
       if (ev) (void)hipEventDestroy(ev);
   if (c->ev_sum) (void)hipEventDestroy(c->ev_sum);
@@ -812,6 +797,46 @@ int qmfx_group_signals(qmfx_ctx* c, const void* records, int64_t nnz, int64_t* n
     if (int rc = build_buckets(c, side)) return rc;
   if (nusers) *nusers = c->s[0].n;
   if (nitems) *nitems = c->s[1].n;
+  return 0;
+}
+
+int qmfx_import_signals(qmfx_ctx* dst, qmfx_ctx* src) {
+  if (!dst || !src || dst == src) return fail("qmfx_import_signals: two distinct contexts needed");
+  if (dst->prec != src->prec) return fail("qmfx_import_signals: contexts differ in precision");
+  for (int side = 0; side < 2; ++side) {
+    const SideBuf& s = src->s[side];
+    if (!s.rowptr || !s.col || s.h_rowptr.empty()) return fail("qmfx_import_signals: the source has no CSR");
+    if (s.sharded) return fail("qmfx_import_signals: the source CSR is sharded");
+  }
+  if (int rc = qmfx_set_shape(dst, src->s[0].n, src->s[1].n)) return rc;
+  if (set_dev(dst)) return -2;
+  for (int side = 0; side < 2; ++side) {
+    const SideBuf& s = src->s[side];
+    SideBuf& d = dst->s[side];
+    drop_csr(d, true);
+    const size_t m = (size_t)std::max<int64_t>(s.nnz, 1);
+    HIPCHK(hipMalloc(&d.rowptr, (size_t)(s.n + 1) * sizeof(int64_t)));
+    HIPCHK(hipMalloc(&d.col, m * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&d.val, m * dst->esz));
+    // device to device over xGMI (the same device: a plain copy)
+    HIPCHK(hipMemcpyPeerAsync(d.rowptr, dst->device, s.rowptr, src->device,
+                              (size_t)(s.n + 1) * sizeof(int64_t), dst->stream));
+    if (s.nnz > 0) {
+      HIPCHK(hipMemcpyPeerAsync(d.col, dst->device, s.col, src->device,
+                                (size_t)s.nnz * sizeof(int32_t), dst->stream));
+      HIPCHK(hipMemcpyPeerAsync(d.val, dst->device, s.val, src->device, (size_t)s.nnz * dst->esz,
+                                dst->stream));
+    }
+    d.nnz = s.nnz;
+    d.h_rowptr = s.h_rowptr;
+    d.h_ids = s.h_ids;
+  }
+  HIPCHK(hipStreamSynchronize(dst->stream));
+  dst->nnz = src->nnz;
+  for (int side = 0; side < 2; ++side) {
+    set_default_bounds(dst->s[side], dst->world, dst->rank);
+    if (int rc = build_buckets(dst, side)) return rc;
+  }
   return 0;
 }
 
@@ -1090,15 +1115,15 @@ int half_piece(qmfx_ctx* c, int j) {
       if (fp32) {
         SolveArgs<float> a{L.rowptr, colp(L), valp<float>(L), (const float*)c->Z, nullptr,
                            (float*)L.F, c->rowloss, c->status, L.d_order, pc.ord + pc.wb[b],
-                           cnt, (float)alpha, (float)lambda, c->k, c->ablate, L.d_desc, nullptr,
+                           cnt, (float)alpha, (float)lambda, c->k, L.d_desc, nullptr,
                            trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
-        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->ksel, c->stream));
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       } else {
         SolveArgs<double> a{L.rowptr, colp(L), valp<double>(L), (const double*)c->Z,
                             nullptr, (double*)L.F, c->rowloss, c->status, L.d_order,
-                            pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, c->ablate, L.d_desc,
+                            pc.ord + pc.wb[b], cnt, alpha, lambda, c->k, L.d_desc,
                             nullptr, trace_path ? c->trace : nullptr, (int32_t)c->z_cap};
-        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->ksel, c->stream));
+        HIPCHK(launch_wals_woodbury(a, c->nt, b + 1, c->stream));
       }
     }
     if (fp32)
@@ -1125,14 +1150,14 @@ int half_piece(qmfx_ctx* c, int j) {
 int half_comm_piece(qmfx_ctx* c, int j) {
   if (set_dev(c)) return -2;
   // fault injection for the clique's failure path (tests): QMFX_FAULT_COMM_RANK=<rank>
-  if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK"))
-    if (c->comm && std::atoi(f) == c->rank) return fail("injected collective failure", -3);
+  if (c->comm && c->fault_comm_rank == c->rank) return fail("injected collective failure", -3);
   SideBuf& L = c->s[c->hs.side];
   const int P = (int)L.pieces.size();
   if (c->comm) {
     // piece j of every rank → every rank (an all-gather-v of contiguous row ranges), on
     // the collective stream while the next piece is solved
     HIPCHK(hipStreamWaitEvent(c->comm_stream, c->evp[j][2], 0));
+    HIPCHK(hipEventRecord(c->evx[j][0], c->comm_stream));
     NCCLCHK(ncclGroupStart());
     for (int r = 0; r < c->world; ++r) {
       const int64_t b = L.pbounds[(size_t)r * (P + 1) + j], e = L.pbounds[(size_t)r * (P + 1) + j + 1];
@@ -1142,6 +1167,7 @@ int half_comm_piece(qmfx_ctx* c, int j) {
                             c->comm_stream));
     }
     NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(c->evx[j][1], c->comm_stream));
   }
   return 0;
 }
@@ -1210,6 +1236,21 @@ int half_end(qmfx_ctx* c, double* loss_sum) {
   HIPCHK(hipEventElapsedTime(&ms_h, c->evh[0], c->evh[2]));
   const double k = c->k, s = (double)c->esz;
   const int sd = c->hs.side;
+  if (c->comm) {
+    // the exchange on the collective stream (the status all-reduce behind the last piece's
+    // broadcasts has completed: the host synchronised on it above)
+    float xb = 0.f, tail = 0.f;
+    for (int j = 0; j < P; ++j) {
+      float t = 0.f;
+      HIPCHK(hipEventElapsedTime(&t, c->evx[j][0], c->evx[j][1]));
+      xb += t;
+    }
+    HIPCHK(hipEventElapsedTime(&tail, c->evp[P - 1][2], c->evx[P - 1][1]));
+    c->xch_ms[sd] += xb;
+    c->xch_tail_ms[sd] += tail;
+    c->xch_solve_ms[sd] += ms_d + ms_w;
+    c->xch_halves[sd] += 1;
+  }
   auto acc = [&](int cls, double ms, double fl, double by) {
     c->cls_ms[cls] += ms;
     c->cls_launches[cls] += 1;
@@ -1568,6 +1609,8 @@ int qmfx_bpr_epoch(qmfx_ctx* c, uint64_t seed, int num_neg, double lr, double bi
     a.seed = seed;
     a.perm_a = pa;
     a.perm_b = pb;
+    c->bpr_waves = a.waves;
+    c->bpr_atomic_user = a.atomic_user;
     HIPCHK(launch_bpr_epoch_f32(a, c->kp, c->stream));
   } else {
     auto a = bpr_args<double>(c, lr, bias_lambda, user_lambda, item_lambda, use_biases);
@@ -1575,6 +1618,8 @@ int qmfx_bpr_epoch(qmfx_ctx* c, uint64_t seed, int num_neg, double lr, double bi
     a.seed = seed;
     a.perm_a = pa;
     a.perm_b = pb;
+    c->bpr_waves = a.waves;
+    c->bpr_atomic_user = a.atomic_user;
     HIPCHK(launch_bpr_epoch_f64(a, c->kp, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -1896,6 +1941,10 @@ int qmfx_kernel_stats_side(qmfx_ctx* c, int cls, int side, double* total_ms, int
 }
 
 int qmfx_reset_stats(qmfx_ctx* c) {
+  for (int sd = 0; sd < 2; ++sd) {
+    c->xch_ms[sd] = c->xch_tail_ms[sd] = c->xch_solve_ms[sd] = 0;
+    c->xch_halves[sd] = 0;
+  }
   c->solve_ms = c->solve_flops = c->solve_bytes = 0;
   c->solve_launches = 0;
   for (int i = 0; i < 3; ++i) {
@@ -1908,6 +1957,27 @@ int qmfx_reset_stats(qmfx_ctx* c) {
   }
   return 0;
 }
+
+int qmfx_exchange_stats(qmfx_ctx* c, int side, double* exchange_ms, double* exposed_ms,
+                        double* solve_ms, int64_t* halves) {
+  if (side != 0 && side != 1) return fail("side must be 0 or 1");
+  if (exchange_ms) *exchange_ms = c->xch_ms[side];
+  if (exposed_ms) *exposed_ms = c->xch_tail_ms[side];
+  if (solve_ms) *solve_ms = c->xch_solve_ms[side];
+  if (halves) *halves = c->xch_halves[side];
+  return 0;
+}
+
+int qmfx_bpr_plan(qmfx_ctx* c, int* waves, int* atomic_user) {
+  if (waves) *waves = c->bpr_waves;
+  if (atomic_user) *atomic_user = c->bpr_atomic_user;
+  return 0;
+}
+
+// A timing-variant build (tools/build_variant.sh) links an object that defines this; the
+// product library does not, and reports "".
+extern "C" __attribute__((weak)) const char* qmfx_variant_flags_tag(void);
+const char* qmfx_build_variant(void) { return qmfx_variant_flags_tag ? qmfx_variant_flags_tag() : ""; }
 
 int qmfx_selftest_mfma(int device, int precision, const double* A, const double* B, double* C) {
   HIPCHK(hipSetDevice(device));

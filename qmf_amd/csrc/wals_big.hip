@@ -35,15 +35,6 @@
 #ifndef QMFX_BIG_SIG64
 #define QMFX_BIG_SIG64 16
 #endif
-#ifndef QMFX_BIG_PANEL_ALL
-#define QMFX_BIG_PANEL_ALL 1  // every wave factors the panel's diagonal block with its own rows
-#endif
-// fp64 k = 256 on the row-pair tile map (QMFX_BIG_PAIR64=1): half the Gram's LDS reads, but
-// 248 spilled VGPRs against 84 — C5 fp64 item half 1392 → 2175 ms (profiles/r04/
-// ab_big_pair64_c5_f64.txt).  Off by default.
-#ifndef QMFX_BIG_PAIR64
-#define QMFX_BIG_PAIR64 0
-#endif
 #ifndef QMFX_BIG_SPLIT
 #define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
 #endif
@@ -54,20 +45,17 @@ template <typename T, int NT>
 struct BigCfg {
   static constexpr int KP = 16 * NT;
   static constexpr int NTT = NT * (NT + 1) / 2;
-  // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave
-#ifndef QMFX_BIG_NW64_8
-#define QMFX_BIG_NW64_8 4  // waves per row at fp64 k ≤ 128 (only with QMFX_F64_BIG=1)
-#endif
-  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? QMFX_BIG_NW64_8 : 8);
+  // waves per row: ≤ 17 fp32 / ≤ 10 fp64 accumulator tiles per wave (fp64 NT ≤ 8: the tiled
+  // YᵀY only; those rows run the one-wave direct kernel)
+  static constexpr int NW = sizeof(T) == 4 ? (NT <= 10 ? 4 : QMFX_BIG_NW32) : (NT <= 8 ? 4 : 8);
   // split-bf16 Gram (fp32, NT = 2·NW): the loader threads split each staged element once
   // into bf16 hi/mid/lo planes ([column][signal], 32 signals = one 16x16x32 MFMA K step)
   // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
   // planes once per stage for both rows
   static constexpr bool SPLIT = sizeof(T) == 4 && NT == 2 * NW && QMFX_BIG_SPLIT;
   // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles) for the split Gram
-  // and for fp64 k = 256, whose Gram then reads each column block once per step for both
-  // rows (17 LDS reads per 17 MFMAs instead of 34 with the round-robin map)
-  static constexpr bool PAIR = SPLIT || (sizeof(T) == 8 && NT == 2 * NW && QMFX_BIG_PAIR64);
+  // (fp64 k = 256 on this map spilled 248 VGPRs against 84: round 4, tools/exp)
+  static constexpr bool PAIR = SPLIT;
   static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
@@ -144,68 +132,6 @@ __device__ __forceinline__ void dispatch_wave(int wv, F&& f) {
   }
 }
 
-// Panel p of the right-looking Cholesky.  Rows 16p..KP-1 of column block p are in S.panel
-// (row q at q·PLD), the right-hand side in S.bw.  Head (one wave): rows 0..63 of the panel —
-// factors the 16×16 diagonal block (L, 1/diag in S.invd), solves the 48 rows below it,
-// applies the forward substitution to b and keeps the diagonal block in S.Ldiag.
-template <typename T, int NT>
-__device__ void big_panel_head(BigShared<T, NT>& S, int p, int lane, int& bad) {
-  constexpr int KP = 16 * NT;
-  constexpr int PLD = BigCfg<T, NT>::PLD;
-  const int R = KP - 16 * p;
-  const int q = lane;
-  const bool live = q < R;
-  T pa[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
-  T pb = live ? S.bw[16 * p + q] : T(0);
-  // as chol_solve's panel (wals.hip): the column's entries A[m][c] of the diagonal block are
-  // broadcast before the pivot is known (L[q][c]·L[m][c] = (A[q][c]/d)·A[m][c]), 1/√d comes
-  // from one reciprocal square root, and 1/L[c][c], y_c stay in lane c until the end
-  T invv = T(0), yv = T(0);
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    T am[16];
-#pragma unroll
-    for (int m = 1; m < 16; ++m)
-      if (m > c) am[m] = readlane(pa[c], m);
-    const T d = readlane(pa[c], c);
-    const T bc = readlane(pb, c);
-    T ljj, inv;
-    pivot_sqrt(d, ljj, inv);
-    (void)ljj;
-    bad |= !(d > T(0));
-    const bool me = lane == c;
-    invv = me ? inv : invv;
-    yv = me ? bc * inv : yv;
-    // rows below take L[q][c] = A[q][c]/√d (the pivot row √d; rows above: dead upper part)
-    const T lq = pa[c] * inv;
-    const T lqs = lq * inv;
-    pa[c] = lq;
-    pb -= lqs * bc;
-#pragma unroll
-    for (int m = 1; m < 16; ++m)
-      if (m > c) pa[m] -= lqs * am[m];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (lane < 16) {
-    S.invd[16 * p + lane] = invv;
-    S.bw[16 * p + lane] = yv;
-    S.yd[16 * p + lane] = yv;
-  }
-  if (live) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
-    if (q >= 16) S.bw[16 * p + q] = pb;
-  }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int idx = lane; idx < 256; idx += 64) {
-    const int r = idx >> 4, c = idx & 15;
-    S.Ldiag[(p * 16 + r) * PLD + c] = c <= r ? S.panel[r * PLD + c] : T(0);
-  }
-}
-
 // Panel p on every wave at once: lanes 0..15 of each wave hold the diagonal block (factored
 // redundantly, as in the head), lanes 16..63 rows 48W + 16 .. 48W + 63 of the panel; each
 // wave runs the head's column loop on its own rows, so the serial head and the slot phase
@@ -215,7 +141,7 @@ __device__ void big_panel_all(BigShared<T, NT>& S, int p, int wv, int lane, int&
   constexpr int KP = 16 * NT;
   constexpr int PLD = BigCfg<T, NT>::PLD;
   const int R = KP - 16 * p;
-  static_assert(48 * BigCfg<T, NT>::NW + 16 >= KP || !QMFX_BIG_PANEL_ALL, "panel rows beyond the waves' lanes");
+  static_assert(48 * BigCfg<T, NT>::NW + 16 >= KP, "panel rows beyond the waves' lanes");
   if (wv > 0 && 48 * wv + 16 >= R) return;  // no rows below the diagonal block for this wave
   const int q = lane < 16 ? lane : 48 * wv + lane;
   const bool live = q < R;
@@ -261,35 +187,6 @@ __device__ void big_panel_all(BigShared<T, NT>& S, int p, int wv, int lane, int&
     S.yd[16 * p + lane] = yv;
 #pragma unroll
     for (int c = 0; c < 16; ++c) S.Ldiag[(p * 16 + lane) * PLD + c] = c <= lane ? pa[c] : T(0);
-  }
-}
-
-// Rows base..base+63 of panel p (base ≥ 64), after the head: L(q, :) = A(q, :) · L_diag⁻ᵀ
-// column by column and b(q) −= L(q, c)·y_c.  Independent rows: the slots of a panel run on
-// different waves at once.
-template <typename T, int NT>
-__device__ void big_panel_slot(BigShared<T, NT>& S, int p, int base, int lane) {
-  constexpr int KP = 16 * NT;
-  constexpr int PLD = BigCfg<T, NT>::PLD;
-  const int R = KP - 16 * p;
-  const int q = base + lane;
-  const bool live = q < R;
-  T pa[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) pa[c] = live ? S.panel[q * PLD + c] : T(0);
-  T pb = live ? S.bw[16 * p + q] : T(0);
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const T lq = pa[c] * S.invd[16 * p + c];
-    pa[c] = lq;
-    pb -= lq * S.bw[16 * p + c];
-#pragma unroll
-    for (int m = c + 1; m < 16; ++m) pa[m] -= lq * S.Ldiag[(p * 16 + m) * PLD + c];
-  }
-  if (live) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) S.panel[q * PLD + c] = pa[c];
-    S.bw[16 * p + q] = pb;
   }
 }
 
@@ -507,7 +404,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       }
     };
     const int nstages = (int)((end - beg + SIG - 1) / SIG);
-    if (nstages > 0 && !(a.ablate & 1)) {
+    if (nstages > 0) {
       load_meta(beg);
       load_rows();
       store_split(0);
@@ -583,7 +480,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   };
 
   const int nstages = (int)((end - beg + SIG - 1) / SIG);
-  if (nstages > 0 && !(a.ablate & 1)) {
+  if (nstages > 0) {
     load_cols(beg);
     load_rows();
     load_meta(beg);
@@ -608,28 +505,6 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       static_assert(NW == 2 || NW == 4 || NW == 8 || NW == 16, "wave count");
       if constexpr (C::REUSE) {
         dispatch_wave<NW>(wv, gram_stage);
-      } else if constexpr (C::PAIR) {
-        // rows A = W and B = NT−1−W: column block J's fragment serves tiles (B, J) and (A, J)
-        auto pair_stage = [&](auto wtag) __attribute__((always_inline)) {
-          constexpr int W = decltype(wtag)::value, A = W, B = NT - 1 - W;
-#pragma unroll 1
-          for (int k4 = 0; k4 < SIG; k4 += 4) {
-            const T* yk = sg + (k4 + kk) * KP + cl;
-            const T wk = S.w[buf][k4 + kk];
-            const T ya = yk[16 * A], yb = yk[16 * B];
-#pragma unroll
-            for (int J = 0; J <= B; ++J) {
-              const T yj = J == A ? ya : (J == B ? yb : yk[16 * J]);
-              const T wyj = wk * yj;
-              acc[W + 1 + J] = M::mma(yb, wyj, acc[W + 1 + J]);  // tile (B, J)
-              if (J <= A) acc[J] = M::mma(ya, wyj, acc[J]);     // tile (A, J)
-              // a few fragments in flight at a time (hoisting every load of the step
-              // spilled ~300 VGPRs beside the 136 accumulator registers)
-              if ((J & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        };
-        dispatch_wave<NW>(wv, pair_stage);
       } else {
 #pragma unroll 2
         for (int k4 = 0; k4 < SIG; k4 += 4) {
@@ -699,18 +574,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
       }
     }
     __syncthreads();
-    if (!(a.ablate & 2)) {
-#if QMFX_BIG_PANEL_ALL
-      big_panel_all<T, NT>(S, p, wv, lane, bad);
-#else
-      if (wv == 0) big_panel_head<T, NT>(S, p, lane, bad);
-      if (KP - 16 * p > 64) {
-        __syncthreads();
-        for (int base = 64 * (1 + wv); base < KP - 16 * p; base += 64 * NW)
-          big_panel_slot<T, NT>(S, p, base, lane);
-      }
-#endif
-    }
+    big_panel_all<T, NT>(S, p, wv, lane, bad);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {
@@ -723,14 +587,14 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     if constexpr (!C::REUSE) {
 #pragma unroll
       for (int s = 0; s < TPW; ++s) {
-        if (TJ[s] > p && !(a.ablate & 4)) {
+        if (TJ[s] > p) {
           const T* li = S.panel + (16 * (TI[s] - p) + cl) * PLD + kk;
           const T* lj = S.panel + (16 * (TJ[s] - p) + cl) * PLD + kk;
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[s] = M::mma(-li[4 * q], lj[4 * q], acc[s]);
         }
       }
-    } else if (!(a.ablate & 4) && p + 1 < NT) {
+    } else if (p + 1 < NT) {
       auto trailing = [&](auto wtag) {
         big_trailing<T, NT, decltype(wtag)::value>(acc, S.panel, p, cl, kk);
       };
@@ -743,7 +607,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   __syncthreads();
 
   // ---- backward solve Lᵀ x = y ----------------------------------------------------------
-  for (int I = NT - 1; I >= 0 && !(a.ablate & 8); --I) {
+  for (int I = NT - 1; I >= 0; --I) {
     T part = T(0);
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {
@@ -1025,14 +889,27 @@ hipError_t launch_heavy_reduce_big(double* part, double* partb, double* partc, c
     default: return hipErrorInvalidValue; \
   }
 
+// the row kernel takes k > 128 only (qmfx.cpp use_big_rows); the tiled YᵀY also fp64 k = 80..128
+#define QMFX_BIG_ROW_SWITCH(NTV, CALL)    \
+  switch (NTV) {                          \
+    case 9: return CALL(9);               \
+    case 10: return CALL(10);             \
+    case 11: return CALL(11);             \
+    case 12: return CALL(12);             \
+    case 13: return CALL(13);             \
+    case 14: return CALL(14);             \
+    case 15: return CALL(15);             \
+    case 16: return CALL(16);             \
+    default: return hipErrorInvalidValue; \
+  }
 hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s) {
 #define CALL(N) launch_big_nt<float, N>(a, s)
-  QMFX_BIG_SWITCH(nt, CALL)
+  QMFX_BIG_ROW_SWITCH(nt, CALL)
 #undef CALL
 }
 hipError_t launch_wals_big(const SolveArgs<double>& a, int nt, hipStream_t s) {
 #define CALL(N) launch_big_nt<double, N>(a, s)
-  QMFX_BIG_SWITCH(nt, CALL)
+  QMFX_BIG_ROW_SWITCH(nt, CALL)
 #undef CALL
 }
 template <typename T>

@@ -8,7 +8,6 @@
 #include <cstdlib>
 
 #include "chol.h"
-#include "chol4.h"
 #include "common.h"
 #include "kernels.h"
 #include "ntswitch.h"
@@ -31,9 +30,6 @@ namespace qmfx {
 #endif
 #ifndef QMFX_WB3_MIN_WAVES
 #define QMFX_WB3_MIN_WAVES 2
-#endif
-#ifndef QMFX_WB_SPLIT
-#define QMFX_WB_SPLIT 1
 #endif
 template <typename T, int NTK, int NTN, bool TRACE>
 __global__ __launch_bounds__(64, NTK > 8 ? 1 : (NTN == 4 ? QMFX_WB4_MIN_WAVES : (NTN == 3 ? QMFX_WB3_MIN_WAVES : 2)))
@@ -88,35 +84,7 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
   acc_t acc[NTT];
 #pragma unroll
   for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
-  if constexpr (sizeof(T) == 4 && QMFX_WB_SPLIT) {
-    // fp32: 32-deep chunks on the bf16 matrix cores, exact 3-way split (see split3):
-    // chunk s takes the lane's columns q = 2s, 2s+1 (8 values) as its k-slice
-    constexpr int NS = (NTK + 1) / 2;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      Split3 sp[NTN];
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        float x[8];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          x[c4] = zr[I][2 * s][c4];
-          x[4 + c4] = (2 * s + 1 < NTK) ? zr[I][(2 * s + 1) % NTK][c4] : 0.f;
-        }
-        split3(x, sp[I]);
-      }
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-#pragma unroll
-        for (int J = 0; J <= I; ++J) {
-          const int t = tile_index(I, J);
-          acc[t] = mma_split6(sp[I], sp[J], acc[t]);
-        }
-      }
-      // one chunk's splits live at a time (keeps the NTN = 3 kernel at 3 waves/SIMD)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
+  {
 #pragma unroll
     for (int q = 0; q < NTK; ++q) {
 #pragma unroll
@@ -637,12 +605,6 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 #ifndef QMFX_WB64_LTP
 #define QMFX_WB64_LTP 1
 #endif
-#ifndef QMFX_WB64_PRIO
-#define QMFX_WB64_PRIO 0  // s_setprio level of the n×n factorization (timing experiments)
-#endif
-#ifndef QMFX_WB64_PRIOK
-#define QMFX_WB64_PRIOK 0  // s_setprio level of the K pass (timing experiments)
-#endif
 // waves per SIMD the streamed fp64 kernel is compiled for, by n×n tile count (n ≤ 16·NTN)
 #ifndef QMFX_WB64_WAVES
 #define QMFX_WB64_WAVES 2
@@ -764,32 +726,7 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
       buf[I][0] = u[0], buf[I][1] = u[1], buf[I][2] = v[0], buf[I][3] = v[1];
     }
   };
-#if QMFX_EXP_XL2
-  // timing experiment (wrong results): the x' pass gathers from 1024 rows that stay in L2
-  const f64x2* zx[NTN];
-#pragma unroll
-  for (int I = 0; I < NTN; ++I) {
-    const int ce = __shfl(cr[I >> 2], (16 * I + cl) & 63, 64);
-    zx[I] = reinterpret_cast<const f64x2*>(a.Y + (uint64_t)((uint32_t)ce & 1023u) * KP);
-  }
-  auto load_chunk_x = [&](int s, double (&buf)[NTN][4]) {
-    const int c2 = 8 * s + 2 * kk;
-#pragma unroll
-    for (int I = 0; I < NTN; ++I) {
-      const f64x2 u = zx[I][c2], v = zx[I][c2 + 1];
-      buf[I][0] = u[0], buf[I][1] = u[1], buf[I][2] = v[0], buf[I][3] = v[1];
-    }
-  };
-#elif QMFX_EXP_NOX
-  // timing experiment (wrong results): no x' gather at all
-  auto load_chunk_x = [&](int s, double (&buf)[NTN][4]) {
-#pragma unroll
-    for (int I = 0; I < NTN; ++I)
-      for (int c = 0; c < 4; ++c) buf[I][c] = (double)(s + I + c) * 1e-3;
-  };
-#else
   auto load_chunk_x = load_chunk;
-#endif
 
   acc_t acc[NTT];
 #pragma unroll
@@ -799,7 +736,6 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
   for (int I = 0; I < NTN; ++I) sq[I] = 0.0;
   constexpr int KEEP = wb64_keep<NTK, NTN>();
   double keep[KEEP > 0 ? KEEP : 1][NTN][4];
-  if constexpr (QMFX_WB64_PRIOK > 0) __builtin_amdgcn_s_setprio(QMFX_WB64_PRIOK);
   {
     // a ring of KD + 1 chunk buffers: chunk s + KD is in flight while chunk s is consumed
     // (the loop unrolls fully, so every ring index is a compile-time constant)
@@ -854,7 +790,6 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
     }
   }
 
-  if constexpr (QMFX_WB64_PRIOK > 0) __builtin_amdgcn_s_setprio(0);
   double xb = 0.0;
   double ul[NTN], cv[NTN];
   // the n×n system: one factorization for both forms (a copy per form pushed the n = 64
@@ -920,16 +855,7 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
     if (lane + 64 * h < 16 * NTN) S.bw[lane + 64 * h] = rhs[h];
   __syncthreads();
   if (TRACE) tr[2] = __builtin_amdgcn_s_memtime();
-#if QMFX_EXP_NOCHOL
-  // timing experiment (wrong results): no n×n factorization
-  if (lane < 16 * NTN) S.xs[lane] = S.bw[lane];
-  __syncthreads();
-#else
-  // the factorization's dependent chain first when another row shares the SIMD
-  if constexpr (QMFX_WB64_PRIO > 0) __builtin_amdgcn_s_setprio(QMFX_WB64_PRIO);
   row_chol<double, NTN>(acc, S, lane, bad);
-  if constexpr (QMFX_WB64_PRIO > 0) __builtin_amdgcn_s_setprio(0);
-#endif
   if (TRACE) tr[3] = __builtin_amdgcn_s_memtime();
   if (!hasQ) {
     double xbl = 0.0;
@@ -1036,275 +962,6 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
     o[5] = hw | ((uint64_t)xcc << 32);
     o[6] = (uint64_t)n;
     o[7] = (uint64_t)row;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Whitened row kernel, multi-wave: the same n×n solve as wals_woodbury_kernel for factor
-// counts whose whitened rows do not fit one wave's registers (fp64 k > 64, fp32 k = 256).
-// One workgroup of NWK waves per row; wave w holds the column blocks q = w·KW .. w·KW+KW-1
-// of the row's whitened rows Zₛ (same per-lane MFMA operand order as the one-wave kernel),
-// so each wave gathers 1/NWK of every signal's row and computes K = Zₛ Zₛᵀ over its columns.
-// The partial K tiles are summed in fixed order ((w0 + w2) + (w1 + w3)) through LDS into
-// wave 0, which solves the n×n system alone (chol_solve with wave-local LDS ordering); u
-// goes back through LDS and every wave forms x' = Zₛᵀu for its own columns.
-// ---------------------------------------------------------------------------------------
-#ifndef QMFX_MW_F64_NTN4_DEFAULT
-#define QMFX_MW_F64_NTN4_DEFAULT 2
-#endif
-#ifndef QMFX_MW_NWK
-// waves per row of the multi-wave whitened kernel (2 beats 4 at fp64 k = 128, 421 -> 314 ms
-// per C3 user half, and the one-wave kernel at fp32 k = 256, 193 -> 167 ms per C5 user half:
-// twice the rows in flight per CU, one idle wave during the n×n solve instead of three)
-#define QMFX_MW_NWK 2
-#endif
-template <typename T, int NTK, int NTN, int NWK>
-struct MwCfg {
-  static constexpr int KW = (NTK + NWK - 1) / NWK;  // column blocks of 16 per wave
-  static constexpr int NTT = NTN * (NTN + 1) / 2;
-};
-
-template <typename T, int NTK, int NTN, int NWK>
-__global__ __launch_bounds__(64 * NWK, 2) void wals_woodbury_mw_kernel(SolveArgs<T> a) {
-  using M = Mfma<T>;
-  using acc_t = typename M::acc_t;
-  using v4 = typename M::acc_t;
-  using C = MwCfg<T, NTK, NTN, NWK>;
-  constexpr int KP = 16 * NTK;
-  constexpr int KW = C::KW;
-  constexpr int NTT = C::NTT;
-  static_assert(NWK == 2 || NWK == 4, "wave count");  // the K reduction tree
-  __shared__ __attribute__((aligned(16))) CholShared<T, NTN> S;
-  __shared__ __attribute__((aligned(16))) acc_t red[NWK / 2][NTT][64];
-  __shared__ T gq[NWK][16 * NTN];
-  __shared__ double xbp[NWK];
-  __shared__ int sbad;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cl = lane & 15;
-  const int kk = lane >> 4;
-  const RowDesc dn = a.desc[a.row_begin + blockIdx.x];
-  const int64_t row = dn.row;
-  const int n = dn.n;  // ≤ 16·NTN by bucketing
-
-  // signal e = lane (every wave holds the same copy)
-  const bool mine = lane < n;
-  const int cr = mine ? a.col[dn.beg + lane] : a.zrow;
-  const T vr = mine ? a.val[dn.beg + lane] : T(0);
-  const T wl = mine ? a.alpha * vr : T(0);
-  const T cwl = mine ? T(1) + a.alpha * vr : T(0);
-  const bool isP = mine && wl > T(0);
-  const bool isQ = mine && wl == T(0);
-  const uint64_t mQ = __ballot(isQ);
-  const uint64_t mP = __ballot(isP);
-  const bool hasQ = mQ != 0;
-
-  // this wave's column blocks of Zₛ: zr[I][j] = z_{16I+cl}[16q + 4kk .. +3], q = wv·KW + j
-  v4 zr[NTN][KW];
-#pragma unroll
-  for (int I = 0; I < NTN; ++I) {
-    const int ce = __shfl(cr, 16 * I + cl, 64);
-    const v4* zrow = reinterpret_cast<const v4*>(a.Y + (uint64_t)(uint32_t)ce * KP) + kk;
-#pragma unroll
-    for (int j = 0; j < KW; ++j) {
-      const int q = wv * KW + j;
-      zr[I][j] = q < NTK ? zrow[4 * q] : v4{};
-    }
-  }
-  // partial K over this wave's columns
-  acc_t acc[NTT];
-#pragma unroll
-  for (int t = 0; t < NTT; ++t) acc[t] = acc_t{0, 0, 0, 0};
-  if constexpr (sizeof(T) == 4) {
-    constexpr int NS = (KW + 1) / 2;
-#pragma unroll
-    for (int s2 = 0; s2 < NS; ++s2) {
-      Split3 sp[NTN];
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        float x[8];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          x[c4] = zr[I][2 * s2][c4];
-          x[4 + c4] = (2 * s2 + 1 < KW) ? zr[I][(2 * s2 + 1) % KW][c4] : 0.f;
-        }
-        split3(x, sp[I]);
-      }
-#pragma unroll
-      for (int I = 0; I < NTN; ++I)
-#pragma unroll
-        for (int J = 0; J <= I; ++J) acc[tile_index(I, J)] = mma_split6(sp[I], sp[J], acc[tile_index(I, J)]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < KW; ++j)
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp)
-#pragma unroll
-        for (int I = 0; I < NTN; ++I)
-#pragma unroll
-          for (int J = 0; J <= I; ++J)
-            acc[tile_index(I, J)] = M::mma(zr[I][j][comp], zr[J][j][comp], acc[tile_index(I, J)]);
-  }
-  // kq_e = z_eᵀ Σ_{f∈Q} z_f over this wave's columns (general rows only)
-  if (hasQ) {
-    T gpart[KW][4];
-#pragma unroll
-    for (int j = 0; j < KW; ++j)
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp) gpart[j][comp] = T(0);
-#pragma unroll
-    for (int I = 0; I < NTN; ++I) {
-      const bool qe = (mQ >> (16 * I + cl)) & 1;
-#pragma unroll
-      for (int j = 0; j < KW; ++j)
-#pragma unroll
-        for (int comp = 0; comp < 4; ++comp)
-          if (qe) gpart[j][comp] += zr[I][j][comp];
-    }
-#pragma unroll
-    for (int j = 0; j < KW; ++j) row16_sum4(gpart[j]);
-#pragma unroll
-    for (int I = 0; I < NTN; ++I) {
-      T sq = T(0);
-#pragma unroll
-      for (int j = 0; j < KW; ++j)
-#pragma unroll
-        for (int comp = 0; comp < 4; ++comp) sq += zr[I][j][comp] * gpart[j][comp];
-      sq += shfl_xor(sq, 16);
-      sq += shfl_xor(sq, 32);
-      if (kk == 0) gq[wv][16 * I + cl] = sq;
-    }
-  }
-  // fixed-order reduction of the K partials into wave 0: ((w0 + w2) + (w1 + w3))
-#pragma unroll
-  for (int h = NWK / 2; h >= 1; h /= 2) {
-    if (wv >= h && wv < 2 * h) {
-#pragma unroll
-      for (int t = 0; t < NTT; ++t) red[wv - h][t][lane] = acc[t];
-    }
-    __syncthreads();
-    if (wv < h) {
-#pragma unroll
-      for (int t = 0; t < NTT; ++t) acc[t] += red[wv][t][lane];
-    }
-    __syncthreads();
-  }
-
-  double xb = 0.0;
-  if (wv == 0) {
-    int bad = __any(mine && wl < T(0)) ? 1 : 0;  // negative confidence: not SPD in this form
-    T rhs;
-    if (!hasQ) {
-      // every real signal in P: S = W⁻¹ + K, identity on padding slots
-      const T iw = isP ? fast_rcp(wl) : T(1);
-      rhs = isP ? cwl * iw : T(0);
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        const T iwd = __shfl(iw, 16 * I + cl, 64);
-        const int t = tile_index(I, I);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][r] += M::crow(lane, r) == cl ? iwd : T(0);
-      }
-    } else {
-      // (W_P⁻¹ + K_PP) u_P = W_P⁻¹ c_P − K_PQ 1_Q,  u_Q = 1
-      rhs = isP ? cwl * fast_rcp(wl) : T(0);
-      if (lane < 16 * NTN) {
-        T kq = T(0);
-#pragma unroll
-        for (int w = 0; w < NWK; ++w) kq += gq[w][lane];
-        if (isP) rhs -= kq;
-      }
-      const T iw = isP ? fast_rcp(wl) : T(0);
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        const T iwd = __shfl(iw, 16 * I + cl, 64);
-#pragma unroll
-        for (int J = 0; J <= I; ++J) {
-          const int t = tile_index(I, J);
-          const int f = 16 * J + cl;
-          const bool pf = (mP >> f) & 1;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int e = 16 * I + M::crow(lane, r);
-            const bool pe = (mP >> e) & 1;
-            T v = acc[t][r];
-            if (pe && pf) v += (e == f) ? iwd : T(0);
-            else v = (e == f) ? T(1) : T(0);
-            acc[t][r] = v;
-          }
-        }
-      }
-    }
-    if (lane < 16 * NTN) S.bw[lane] = rhs;
-    csync<true>();
-    chol_solve<T, NTN, true>(acc, S, lane, bad);
-    if (!hasQ) {
-      // xᵀb = Σ_e (c_e/w_e)(c_e − u_e)
-      const T ue = lane < 16 * NTN ? S.xs[lane] : T(0);
-      xb = wave_sum(isP ? (double)(rhs * (cwl - ue)) : 0.0);
-    }
-    if (lane == 0) sbad = bad;
-  }
-  __syncthreads();
-  // every wave: u of its lane's signals, x' = Zₛᵀu over its columns
-  T ul[NTN], cv[NTN];
-#pragma unroll
-  for (int I = 0; I < NTN; ++I) {
-    const int e = 16 * I + cl;
-    const bool pe = (mP >> e) & 1;
-    const bool qe = (mQ >> e) & 1;
-    ul[I] = hasQ ? (pe ? S.xs[e] : (qe ? T(1) : T(0))) : S.xs[e];
-    cv[I] = __shfl(cwl, e, 64);
-  }
-  const bool bad = sbad != 0;
-  double xbw = 0.0;
-#pragma unroll
-  for (int j = 0; j < KW; ++j) {
-    const int q = wv * KW + j;
-    T xq[4], sb[4];
-#pragma unroll
-    for (int comp = 0; comp < 4; ++comp) {
-      xq[comp] = T(0);
-      sb[comp] = T(0);
-#pragma unroll
-      for (int I = 0; I < NTN; ++I) {
-        xq[comp] += zr[I][j][comp] * ul[I];
-        if (hasQ) sb[comp] += zr[I][j][comp] * cv[I];
-      }
-    }
-    row16_sum4(xq);
-    if (hasQ) {
-      row16_sum4(sb);
-#pragma unroll
-      for (int comp = 0; comp < 4; ++comp) xbw += (double)xq[comp] * (double)sb[comp];
-    }
-    if (q < NTK && cl == j % 16) {
-      v4 o = {xq[0], xq[1], xq[2], xq[3]};
-      if (bad) o = v4{};
-      reinterpret_cast<v4*>(a.X + row * KP)[4 * q + kk] = o;
-    }
-  }
-  if (hasQ) {
-    // xᵀb = x'ᵀ(Zₛᵀc): per-wave partials (one copy per 16-lane row), fixed-order total
-    xbw = wave_sum(cl == 0 ? xbw : 0.0);
-    if (lane == 0) xbp[wv] = xbw;
-    __syncthreads();
-    if (tid == 0) {
-      xb = 0.0;
-#pragma unroll
-      for (int w = 0; w < NWK; ++w) xb += xbp[w];
-    }
-  }
-  if (wv == 0) {
-    const double csum = wave_sum((double)cwl);
-    if (lane == 0) {
-      a.rowloss[row] = bad ? 0.0 : csum - xb;  // −λ‖x‖² added after unwhitening
-      if (bad && a.status) a.status[row] = 1;
-    }
   }
 }
 
@@ -1461,43 +1118,14 @@ __global__ __launch_bounds__(256) void chol_inv_kernel(const T* G, int k, double
 
 
 #ifndef QMFX_KERNELS_ONLY
-static bool env_flag(const char* name, bool dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) != 0 : dflt;
-}
-static int env_int(const char* name, int dflt, int lo, int hi) {
-  const char* e = std::getenv(name);
-  return e ? std::min(std::max(std::atoi(e), lo), hi) : dflt;
-}
-KernelSel read_kernel_sel() {
-  KernelSel k;
-  // fp32 k ≤ 128 and k = 256: the streamed kernel (QMFX_WB_STREAM=0: the register-resident one)
-  k.wb_stream = env_flag("QMFX_WB_STREAM", true);
-  // fp64 k = 80..128: the streamed kernel (QMFX_WB_ST64=0: the multi-wave kernel)
-  k.wb_st64 = env_flag("QMFX_WB_ST64", true);
-  // fp32 k = 256: the streamed one-wave kernel (C5 user half 161 -> 152 ms), or the
-  // multi-wave kernel with QMFX_WB_MW=1
-  k.wb_mw = env_flag("QMFX_WB_MW", false);
-  // fp64 n×n bucket 4 at k = 128 on the multi-wave kernel: 2 waves per row spill 76 VGPRs, 4
-  // waves do not (2 or 4, for comparisons)
-  k.mw_f64_ntn4 = env_int("QMFX_MW_F64_NTN4", QMFX_MW_F64_NTN4_DEFAULT, 2, 4);
-  // largest whitened bucket at fp32 k = 128: n ≤ 128 on the streamed kernel (same-box A/B at
-  // C3: 163.6 -> 158.7 ms/epoch over keeping n > 64 direct; 4 restores that)
-  k.k128_ntn = env_int("QMFX_WB_K128_NTN", 8, 1, 8);
-  // largest whitened bucket at fp64 k = 128: n ≤ 80 on the streamed kernel (4 keeps n > 64
-  // direct)
-  k.f64_ntn = env_int("QMFX_WB_F64_NTN", 5, 1, 5);
-  k.k256_ntn = env_int("QMFX_WB_K256_NTN", 8, 1, 8);  // comparisons: 4 keeps n > 64 direct
-  return k;
-}
-
 template <typename T, int NTK>
-static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, bool stream, hipStream_t s) {
+static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_t s) {
   if (a.nrows <= 0) return hipSuccess;
   if (!a.desc) return hipErrorInvalidValue;
   const dim3 b(64);
-  if constexpr (sizeof(T) == 4 && (NTK <= 8 || NTK == 16)) {
-    if (!a.trace && stream) {
+  // fp32: the streamed kernel (every bucket); fp64 k ≤ 64: the register-resident one
+  if constexpr (sizeof(T) == 4) {
+    {
 #define QMFX_WBS(N)                                                                        \
   return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                             \
     hipLaunchKernelGGL((wals_woodbury_st_kernel<NTK, N>), dim3((unsigned)c.nrows), b, 0, s, c); \
@@ -1530,7 +1158,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, bool strea
       }
 #undef QMFX_WBS
     }
-  }
+  } else {
 #define QMFX_WB(N)                                                                            \
   return launch_row_chunks(a, 64, [&](const SolveArgs<T>& c) {                                \
     if (c.trace)                                                                              \
@@ -1553,40 +1181,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, bool strea
   } else {
     return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-// multi-wave whitened kernel: 4 waves per row (the fp64 n ≤ 64 bucket: ntn4_waves)
-template <typename T, int NTK>
-static hipError_t launch_woodbury_mw_ntk(const SolveArgs<T>& a, int ntn, int ntn4_waves,
-                                         hipStream_t s) {
-  if (a.nrows <= 0) return hipSuccess;
-  if (!a.desc) return hipErrorInvalidValue;
-  constexpr int NWK = QMFX_MW_NWK;
-  if constexpr (sizeof(T) == 8 && NTK >= 8) {
-    if (ntn == 4 && ntn4_waves == 4)
-      return launch_row_chunks(a, 256, [&](const SolveArgs<T>& c) {
-        hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, 4, 4>), dim3((unsigned)c.nrows),
-                           dim3(256), 0, s, c);
-      });
   }
-#define QMFX_WBMW(N)                                                                   \
-  return launch_row_chunks(a, 64 * NWK, [&](const SolveArgs<T>& c) {                   \
-    hipLaunchKernelGGL((wals_woodbury_mw_kernel<T, NTK, N, NWK>), dim3((unsigned)c.nrows), \
-                       dim3(64 * NWK), 0, s, c);                                       \
-  })
-  switch (ntn) {
-    case 1: QMFX_WBMW(1);
-    case 2: QMFX_WBMW(2);
-    case 3:
-      if constexpr (NTK >= 6) QMFX_WBMW(3);
-      return hipErrorInvalidValue;
-    case 4:
-      if constexpr (NTK >= 8) QMFX_WBMW(4);
-      return hipErrorInvalidValue;
-    default: return hipErrorInvalidValue;
-  }
-#undef QMFX_WBMW
 }
 
 template <int NTK>
@@ -1618,12 +1213,6 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
     default: return hipErrorInvalidValue;
   }
 #undef QMFX_WBS64
-}
-
-int whitened_max_ntn_k128(const KernelSel& ks) { return ks.wb_stream ? ks.k128_ntn : 4; }
-int whitened_max_ntn_f64_k128(const KernelSel& ks) { return ks.wb_st64 ? ks.f64_ntn : 4; }
-int whitened_max_ntn_k256(const KernelSel& ks) {
-  return (!ks.wb_stream || ks.wb_mw) ? 4 : ks.k256_ntn;
 }
 
 template <typename T, int NT>
@@ -1711,35 +1300,22 @@ static hipError_t launch_chol_inv_nt(const T* G, int k, double lambda, T* Linv, 
   }
 }
 
-hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, const KernelSel& ks,
-                                hipStream_t s) {
-  if (nt == 16 && ks.wb_mw) return launch_woodbury_mw_ntk<float, 16>(a, ntn, ks.mw_f64_ntn4, s);
-#define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, ks.wb_stream, s)
+hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipStream_t s) {
+#define CALL(N) launch_woodbury_ntk<float, N>(a, ntn, s)
   QMFX_NT_SWITCH_W(nt, CALL)
 #undef CALL
 }
-hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn,
-                                const KernelSel& ks, hipStream_t s) {
-  // one wave up to k = 64; k = 80..128 and 256 on the streamed kernel (QMFX_WB_ST64=0: the
-  // multi-wave one up to k = 128, the big kernel at k = 256)
-  if (((nt >= 5 && nt <= 8) || nt == 16) && ks.wb_st64) {
-    switch (nt) {
-      case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
-      case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
-      case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);
-      case 8: return launch_woodbury_st64_ntk<8>(a, ntn, s);
-      case 16: return launch_woodbury_st64_ntk<16>(a, ntn, s);
-      default: break;
-    }
-  }
+hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
+  // one wave up to k = 64; k = 80..128 and 256 on the streamed fp64 kernel
   switch (nt) {
-    case 5: return launch_woodbury_mw_ntk<double, 5>(a, ntn, ks.mw_f64_ntn4, s);
-    case 6: return launch_woodbury_mw_ntk<double, 6>(a, ntn, ks.mw_f64_ntn4, s);
-    case 7: return launch_woodbury_mw_ntk<double, 7>(a, ntn, ks.mw_f64_ntn4, s);
-    case 8: return launch_woodbury_mw_ntk<double, 8>(a, ntn, ks.mw_f64_ntn4, s);
+    case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
+    case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
+    case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);
+    case 8: return launch_woodbury_st64_ntk<8>(a, ntn, s);
+    case 16: return launch_woodbury_st64_ntk<16>(a, ntn, s);
     default: break;
   }
-#define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, false, s)
+#define CALL(N) launch_woodbury_ntk<double, N>(a, ntn, s)
   QMFX_NT_SWITCH64(nt, CALL)
 #undef CALL
 }

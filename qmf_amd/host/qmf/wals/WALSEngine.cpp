@@ -53,10 +53,9 @@ void WALSEngine::init(const std::vector<DatasetElem>& dataset) {
     QMFX_CHECK(qmfx_get_ids(c, QMFX_ITEMS, iids.data()));
     userIndex_.assignSorted(std::move(uids));
     itemIndex_.assignSorted(std::move(iids));
-    // every rank builds the same CSR on its own device (sharded by qmfx_dist_init_all)
-    for (size_t r = 1; r < ranks_.size(); ++r)
-      QMFX_CHECK(qmfx_group_signals(ranks_[r], dataset.data(),
-                                    static_cast<int64_t>(dataset.size()), &nu, &ni));
+    // the other ranks copy rank 0's CSR device to device over xGMI (one sort, no further
+    // host→device uploads); qmfx_dist_init_all then keeps each rank's shard
+    for (size_t r = 1; r < ranks_.size(); ++r) QMFX_CHECK(qmfx_import_signals(ranks_[r], c));
   } else {
     // beyond the device sort's 32-bit item count: the same grouping on the host
     SignalCsr byUser, byItem;

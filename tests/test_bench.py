@@ -56,3 +56,68 @@ def test_cpu_epoch_estimate_is_conservative_at_c3():
     # measured on the GPU box: 355.5 s on 16 threads (profiles/r02)
     est = bench.cpu_epoch_estimate_s(10_000_000, 1_000_000, 500_000_000, 128, 16)
     assert 355.5 < est < 500
+
+
+def test_work_skipping_env_is_refused():
+    """A work-skipping knob in the environment: no line is printed (SystemExit)."""
+    with pytest.raises(SystemExit, match="QMFX_ABLATE"):
+        bench.check_env({"QMFX_ABLATE": "3"}, "")
+    bench.check_env({"QMFX_ABLATE": "0", "QMFX_PIECES": "4"}, "")  # 0 / route knobs are fine
+
+
+def test_variant_library_is_refused_unless_allowed():
+    with pytest.raises(SystemExit, match="timing-variant"):
+        bench.check_env({}, "exp1: woodbury.hip -DFOO=1")
+    bench.check_env({}, "exp1: woodbury.hip -DFOO=1", allow_variant=True)
+    bench.check_env({}, "")
+
+
+def test_engine_env_reports_qmfx_knobs_only():
+    env = {"QMFX_PIECES": "4", "QMFX_BENCH_LIMIT_S": "60", "PATH": "/bin", "QMFX_NO_WHITEN": "1"}
+    assert bench.engine_env(env) == {"QMFX_NO_WHITEN": "1", "QMFX_PIECES": "4"}
+
+
+def test_product_library_is_not_a_variant():
+    import qmf_amd
+    assert qmf_amd._abi.build_variant() == ""
+
+
+def _exchange_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r: exchange 10+r ms per half (summed over 2 steps), exposed 1+r, solves 20-r
+    stats = {sd: {"exchange_ms": 2 * (10.0 + rank + sd), "exposed_ms": 2 * (1.0 + rank),
+                  "solve_ms": 2 * (20.0 - rank), "halves": 2} for sd in (0, 1)}
+
+    def reduce_max(vals):
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t]
+    q.put((rank, bench.exchange_fields(stats, 2, reduce_max)))
+    dist.destroy_process_group()
+
+
+def test_exchange_fields_are_max_over_ranks_gloo_world2():
+    """--gpus N lines carry per-half exchange_ms / exposed_ms / solve_ms, the max over ranks
+    (the driver's first 8-GPU run must say whether the user half is exchange-bound)."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_exchange_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    f = res[0]
+    assert set(f) == {"user_half", "item_half"}
+    assert f["user_half"] == {"exchange_ms": 11.0, "exposed_ms": 2.0, "solve_ms": 20.0}
+    assert f["item_half"] == {"exchange_ms": 12.0, "exposed_ms": 2.0, "solve_ms": 20.0}

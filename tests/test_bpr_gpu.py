@@ -74,7 +74,12 @@ def triplets(users, items, nitems, seed, num_neg, shuffle):
 @pytest.mark.parametrize("precision,tol", [(64, 1e-12), (32, 1e-5)])
 @pytest.mark.parametrize("use_biases", [False, True])
 @pytest.mark.parametrize("num_neg", [3, 6])
-def test_bpr_epoch_single_wave_exact(precision, tol, use_biases, num_neg):
+@pytest.mark.parametrize("atomic_user", ["0", "1"])
+def test_bpr_epoch_single_wave_exact(precision, tol, use_biases, num_neg, atomic_user,
+                                     monkeypatch):
+    """One wave (the reference's serial order): both ways of writing the user row back (plain
+    store, C4's default; atomic add of the net change, skewed users) are exact."""
+    monkeypatch.setenv("QMFX_BPR_ATOMIC_USER", atomic_user)
     rng = np.random.default_rng(num_neg + 10 * use_biases)
     nu, ni, k = 20, 300, 16
     # user 0 has > 64 positives (rejection scans memory), others a few; few items per
@@ -103,3 +108,30 @@ def test_bpr_epoch_single_wave_exact(precision, tol, use_biases, num_neg):
             assert np.max(np.abs(c.factors(1) - I)) <= tol * scale, epoch
             if use_biases:
                 assert np.max(np.abs(c.bpr_biases() - b)) <= tol * max(np.abs(b).max(), 1), epoch
+            assert c.bpr_plan() == (1, int(atomic_user))
+
+
+@pytest.mark.parametrize("skewed", [False, True])
+def test_bpr_atomic_user_follows_user_skew(skewed):
+    """The user row is stored plainly while concurrent waves rarely hold the same user; a
+    dataset with one dominant user (≥ 1% of the positives per concurrent wave) switches it to
+    the atomic add (qmfx.cpp bpr_args)."""
+    rng = np.random.default_rng(5)
+    # 800 items → 50 concurrent waves; ~50 positives per user (the largest ≈ 80): 50 × 80 <
+    # 1% of ~1M positives.  Skewed: user 0 holds all 800 items
+    nu, ni, k, npos = 20000, 800, 16, 1000000
+    users = rng.integers(0, nu, npos)
+    if skewed:
+        users[: npos // 10] = 0  # one user holds 10% of the positives
+    items = rng.integers(0, ni, npos)
+    keys = np.unique(users * ni + items, return_index=True)[1]
+    users, items = users[np.sort(keys)], items[np.sort(keys)]
+    with qmf_amd.Context(k, 32) as c:
+        c.set_shape(nu, ni)
+        c.fill_uniform(0, 0.01, 1)
+        c.fill_uniform(1, 0.01, 2)
+        c.bpr_set_positives(users, items)
+        c.bpr_epoch(3, 3, 0.05, 1.0, 0.025, 0.0025, False, shuffle=False)
+        waves, atomic = c.bpr_plan()
+    assert waves > 1
+    assert atomic == (1 if skewed else 0)

@@ -15,9 +15,13 @@ pytestmark = pytest.mark.gpu
 LAM, ALPHA = 0.05, 40.0
 
 
-@pytest.mark.parametrize("k,precision,world", [(16, 64, 2), (16, 64, 3), (128, 32, 2),
-                                               (128, 64, 2), (256, 32, 3)])
-def test_partitioned_ranks_assemble_the_full_half(k, precision, world):
+@pytest.mark.parametrize("k,precision,world,ingest", [
+    (16, 64, 2, "upload"), (16, 64, 3, "upload"), (128, 32, 2, "upload"), (128, 64, 2, "upload"),
+    (256, 32, 3, "upload"),
+    # ranks ≥ 1 copy rank 0's CSR device to device (qmfx_import_signals: the drop-in engine's
+    # --ngpus ingest) before sharding
+    (16, 64, 3, "import"), (128, 64, 2, "import")])
+def test_partitioned_ranks_assemble_the_full_half(k, precision, world, ingest):
     u, i, v = synth(3000, 600, 60000, seed=k + world)
     v = v.copy()
     v[::97] = -3.0  # a few indefinite rows: the pivoted re-solve runs on sharded signals
@@ -28,12 +32,18 @@ def test_partitioned_ranks_assemble_the_full_half(k, precision, world):
     ranks = []
     for r in range(world):
         c = qmf_amd.Context(k, precision)
-        c.set_shape(len(uids), len(iids))
-        c.upload_csr(0, *ucsr)
-        c.upload_csr(1, *icsr)
+        if ingest == "import" and r > 0:
+            c.import_signals(ranks[0])
+        else:
+            c.set_shape(len(uids), len(iids))
+            c.upload_csr(0, *ucsr)
+            c.upload_csr(1, *icsr)
         c.set_factors(1, init)
-        c.dist_init(r, world, None)
         ranks.append(c)
+    for r, c in enumerate(ranks):  # rank 0 shards last: the others imported its full CSR
+        if r > 0:
+            c.dist_init(r, world, None)
+    ranks[0].dist_init(0, world, None)
     with pytest.raises(qmf_amd.QmfxError, match="sharded"):
         ranks[0].download_csr(0)
     # fp64: 1e-7, not 1e-9 — the indefinite rows' pivoted solves amplify rounding by cond(A)
@@ -74,11 +84,18 @@ def test_rccl_loopback_matches_plain(k, precision, pieces, monkeypatch):
         if uid is not None:
             c.dist_init(0, 1, uid)
         ctxs.append(c)
+    ctxs[1].reset_stats()
     for _ in range(2):
         for side in (0, 1):
             l0, l1 = (c.wals_half(side, ALPHA, LAM) for c in ctxs)
             assert l0 == l1, side
             assert np.array_equal(ctxs[0].factors(side), ctxs[1].factors(side)), side
+    # the exchange is timed on the collective stream (bench.py --gpus N reports it per half)
+    for side in (0, 1):
+        x = ctxs[1].exchange_stats(side)
+        assert x["halves"] == 2 and x["solve_ms"] > 0, x
+        assert 0 <= x["exposed_ms"] and 0 <= x["exchange_ms"] < 1e4, x
+        assert ctxs[0].exchange_stats(side)["halves"] == 0
     for c in ctxs:
         c.close()
 
@@ -94,11 +111,14 @@ def test_multi_context_driver_matches_plain(k, precision, monkeypatch):
     uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
     init = np.random.default_rng(5).uniform(-0.01, 0.01, (len(iids), k))
     ctxs = []
-    for _ in range(2):
+    for r in range(2):
         c = qmf_amd.Context(k, precision)
-        c.set_shape(len(uids), len(iids))
-        c.upload_csr(0, *ucsr)
-        c.upload_csr(1, *icsr)
+        if r == 0:
+            c.set_shape(len(uids), len(iids))
+            c.upload_csr(0, *ucsr)
+            c.upload_csr(1, *icsr)
+        else:
+            c.import_signals(ctxs[0])  # the --ngpus ingest: one build, device-to-device copies
         c.set_factors(1, init)
         ctxs.append(c)
     qmf_amd.dist_init_all([ctxs[1]])

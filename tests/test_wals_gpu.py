@@ -225,31 +225,24 @@ def test_row_system_matches_oracle():
     assert abs(cs - np.sum(1 + w)) < 1e-9
 
 
-@pytest.mark.parametrize("k,precision,nnz,mw", [
-    (256, 32, 30000, "0"), (128, 32, 30000, "0"), (64, 32, 30000, "0"), (64, 64, 30000, "0"),
-    (32, 64, 30000, "0"),
-    # multi-wave whitened kernel: fp64 k = 80..128, fp32 k = 256 with QMFX_WB_MW=1; the
-    # 160K-signal sets put users at ~40 signals (every n×n bucket up to n = 64)
-    # fp64 k = 80..128 run the streamed fp64 kernel; "st64=0" forces the multi-wave one
-    (128, 64, 30000, "0"), (128, 64, 160000, "0"), (80, 64, 160000, "0"), (112, 64, 160000, "0"),
-    (128, 64, 160000, "st64=0"), (80, 64, 30000, "st64=0"),
-    (256, 32, 160000, "1"), (256, 32, 30000, "1"),
+@pytest.mark.parametrize("k,precision,nnz", [
+    (256, 32, 30000), (128, 32, 30000), (64, 32, 30000), (64, 64, 30000), (32, 64, 30000),
+    # fp64 k = 80..128 run the streamed fp64 kernel; the 160K-signal sets put users at ~40
+    # signals (every n×n bucket up to n = 64)
+    (128, 64, 30000), (128, 64, 160000), (80, 64, 160000), (112, 64, 160000), (80, 64, 30000),
+    (256, 32, 160000),
     # fp32 k = 256 / 128, ~100 signals per user: the n = 65..128 buckets (two signals per
     # lane)
-    (256, 32, 400000, "0"), (128, 32, 400000, "0"),
+    (256, 32, 400000), (128, 32, 400000),
     # fp64 k = 128, ~100 signals per user: the streamed fp64 kernel's n = 65..80 bucket (two
     # signals per lane, second ballot words, 5-tile fp64 Cholesky)
-    (128, 64, 400000, "0"),
+    (128, 64, 400000),
     # fp64 k = 256 (C5 at the reference's precision): the streamed fp64 kernel beside the
     # big k×k kernel, every bucket up to n = 80
-    (256, 64, 30000, "0"), (256, 64, 160000, "0"), (256, 64, 400000, "0")])
-def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatch):
+    (256, 64, 30000), (256, 64, 160000), (256, 64, 400000)])
+def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, monkeypatch):
     """Short rows (n ≤ KP/2) take the whitened n×n path; the same half step with
     QMFX_NO_WHITEN=1 (direct k×k path for every row) and the oracle must agree."""
-    if mw.startswith("st64="):
-        monkeypatch.setenv("QMFX_WB_ST64", mw[5:])
-        mw = "0"
-    monkeypatch.setenv("QMFX_WB_MW", mw)
     u, i, v = synth(4000, 900, nnz, seed=11)  # ~7.5 (or ~40) signals per user
     v[::7] = 0.0  # zero-valued signals (Q set: c = 1, w = 0)
     o, c = make_pair(u, i, v, k, precision, seed=2)
@@ -275,16 +268,14 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, mw, monkeypatc
         cd.set_factors(side, o.factors(side))
 
 
-@pytest.mark.parametrize("k,precision,direct2", [(144, 32, 0), (192, 32, 0), (256, 32, 0),
-                                                 (80, 64, 0), (128, 64, 0), (200, 64, 0), (256, 64, 0),
-                                                 (80, 64, 1), (112, 64, 1), (128, 64, 1)])
-def test_large_k_multiwave_rows(k, precision, direct2, monkeypatch):
+@pytest.mark.parametrize("k,precision", [(144, 32), (192, 32), (256, 32), (80, 64), (112, 64),
+                                         (128, 64), (200, 64), (256, 64)])
+def test_large_k_multiwave_rows(k, precision):
     """k beyond one wave's registers (fp32 > 128, fp64 > 64): the multi-wave row kernel
     (LDS-staged Gram, distributed Cholesky) and the strip YᵀY, against the oracle at the
     reference's λ/α; rows from 1 to ~150 signals cover partial LDS stages and every
-    panel-slot count.  800 items ≫ k keeps the item systems well-posed for fp32.
-    direct2 = 1: fp64 direct rows on the two-wave kernel (QMFX_DIRECT2, wals_direct2.hip)."""
-    monkeypatch.setenv("QMFX_DIRECT2", str(direct2))
+    panel-slot count.  800 items ≫ k keeps the item systems well-posed for fp32.  fp64
+    k = 80..128 rows run the one-wave direct kernel (accumulators across VGPR + AGPR)."""
     u, i, v = synth(4000, 800, 100000, seed=k)
     o, c = make_pair(u, i, v, k, precision, seed=3)
     tol = 1e-9 if precision == 64 else 1e-4

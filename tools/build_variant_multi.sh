@@ -11,7 +11,7 @@ pids=()
 for src in "$@"; do
   extra=""
   [ "$src" = wals_direct_f64 ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
-  /opt/rocm/bin/hipcc $F $extra $flags -Rpass-analysis=kernel-resource-usage -c csrc/$src.hip \
+  /opt/rocm/bin/hipcc $F $extra $flags -Rpass-analysis=kernel-resource-usage -Icsrc -c $( [ -f csrc/$src.hip ] && echo csrc/$src.hip || echo ../tools/exp/$src.hip ) \
     -o $B/var_${name}_$src.o 2> $B/var_${name}_$src.ra &
   pids+=($!)
 done
@@ -19,6 +19,9 @@ for p in "${pids[@]}"; do wait $p; done
 excl=""
 for src in "$@"; do excl="$excl -e /$src.o\$"; done
 OTHERS=$(ls $B/*.o | grep -v $excl -e '/var_')
+# the tag object: qmfx_build_variant() reports this build's flags (bench.py refuses it as the product)
+printf 'extern "C" const char* qmfx_variant_flags_tag(void) { return "%s: %s %s"; }\n' "$name" "$*" "$flags" > $B/var_${name}_tag.cpp
+g++ -O2 -fPIC -c $B/var_${name}_tag.cpp -o $B/var_${name}_tag.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $B/var_$name.so $B/var_${name}_*.o $OTHERS \
   -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -f $B/var_${name}_*.o
+rm -f $B/var_${name}_*.o $B/var_${name}_tag.cpp
