@@ -158,9 +158,10 @@ struct qmfx_ctx {
   double* ev_sq = nullptr;
   double* ev_udbl = nullptr;
   uint64_t bpr_epochs = 0;
-  // QMFX_FAULT_COMM_RANK (tests): the rank whose next piece broadcast fails as if RCCL had
-  // failed, read once at create (-1: none)
+  // QMFX_FAULT_COMM_RANK=<rank>[:<after>] (tests), read once at create: that rank's piece
+  // broadcasts fail as if RCCL had failed once <after> of them have succeeded (-1: none)
   int fault_comm_rank = -1;
+  int64_t fault_comm_after = 0, comm_pieces_done = 0;
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
   // the half-epoch in progress (qmfx_wals_half's phases)
   struct HalfStateT {
@@ -567,7 +568,10 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->kp = 16 * nt;
   c->esz = precision == 32 ? 4 : 8;
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
-  if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK")) c->fault_comm_rank = std::atoi(f);
+  if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK")) {
+    c->fault_comm_rank = std::atoi(f);
+    if (const char* a = std::strchr(f, ':')) c->fault_comm_after = std::atoll(a + 1);
+  }
   if (const char* hm = std::getenv("QMFX_HEAVY_MIN")) c->heavy_min = std::max<int64_t>(std::atoll(hm), 0);
   if (const char* sl = std::getenv("QMFX_SEG_LEN"))
     c->seg_len = std::min<int64_t>(std::max<int64_t>(std::atoll(sl), 64), INT32_MAX);
@@ -1150,7 +1154,8 @@ int half_piece(qmfx_ctx* c, int j) {
 int half_comm_piece(qmfx_ctx* c, int j) {
   if (set_dev(c)) return -2;
   // fault injection for the clique's failure path (tests): QMFX_FAULT_COMM_RANK=<rank>
-  if (c->comm && c->fault_comm_rank == c->rank) return fail("injected collective failure", -3);
+  if (c->comm && c->fault_comm_rank == c->rank && c->comm_pieces_done++ >= c->fault_comm_after)
+    return fail("injected collective failure", -3);
   SideBuf& L = c->s[c->hs.side];
   const int P = (int)L.pieces.size();
   if (c->comm) {

@@ -138,6 +138,8 @@ def test_multi_context_driver_failed_collective_aborts_the_clique(monkeypatch):
     make qmfx_wals_half_multi RETURN the error, with every communicator aborted, and later
     halves on those contexts must fail loudly instead of running or hanging."""
     monkeypatch.setenv("QMFX_PIECES", "2")
+    # read once by the context: rank 0's piece broadcasts fail after the first half's two
+    monkeypatch.setenv("QMFX_FAULT_COMM_RANK", "0:2")
     u, i, v = synth(2000, 400, 30000, seed=8)
     uids, iids, ucsr, icsr = csr_from_triples(u, i, v)
     c = qmf_amd.Context(16, 64)
@@ -147,10 +149,8 @@ def test_multi_context_driver_failed_collective_aborts_the_clique(monkeypatch):
     c.set_factors(1, np.random.default_rng(3).uniform(-0.01, 0.01, (len(iids), 16)))
     qmf_amd.dist_init_all([c])
     qmf_amd.wals_half_multi([c], 0, ALPHA, LAM)  # healthy first
-    monkeypatch.setenv("QMFX_FAULT_COMM_RANK", "0")
     with pytest.raises(qmf_amd.QmfxError, match="injected collective failure"):
         qmf_amd.wals_half_multi([c], 1, ALPHA, LAM)
-    monkeypatch.delenv("QMFX_FAULT_COMM_RANK")
     with pytest.raises(qmf_amd.QmfxError, match="clique was aborted"):
         qmf_amd.wals_half_multi([c], 1, ALPHA, LAM)
     c.close()
