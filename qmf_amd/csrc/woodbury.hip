@@ -628,13 +628,13 @@ constexpr int wb64_kdepth() {
 // SIMD (fp64 whitened rows are bound by the fabric's random-row rate, so every chunk not
 // re-gathered is 1/NTK of the second pass's bytes)
 #ifndef QMFX_WB64_KEEP2
-#define QMFX_WB64_KEEP2 8
+#define QMFX_WB64_KEEP2 6
 #endif
 #ifndef QMFX_WB64_KEEP3
-#define QMFX_WB64_KEEP3 5
+#define QMFX_WB64_KEEP3 2
 #endif
 #ifndef QMFX_WB64_KEEP4
-#define QMFX_WB64_KEEP4 2
+#define QMFX_WB64_KEEP4 1
 #endif
 template <int NTK, int NTN>
 constexpr int wb64_keep() {
