@@ -187,6 +187,66 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
   csum += lane == 0 ? tot : 0.0;  // the caller sums the cl == 0 lanes
 }
 
+// fp64 k = 112 / 128 direct Gram: the accumulator tiles are pinned to a register class by
+// issuing the MFMA from inline asm — the first QMFX_F64_AG tiles in AGPRs (srcC / vdst may be
+// AGPRs at full rate), the rest in VGPRs, so the step's rows, w·y and rhs stay in VGPRs.  With
+// the builtin the allocator put 27 tiles in VGPRs and 9 in AGPRs, landed the gathered rows in
+// AGPRs and copied them (and one rotating tile) through v_accvgpr moves at every step
+// boundary.  The asm is opaque to the hazard recognizer: each MFMA carries its own 2 wait
+// states for a VALU-written srcA/B/C (issued while the previous MFMA holds the pipe), and the
+// loop's exit pads the f64 MFMA → VALU/VMEM read distance (gram_asm_drain).
+#ifndef QMFX_F64_ASM
+#define QMFX_F64_ASM 1
+#endif
+#ifndef QMFX_F64_AG
+#define QMFX_F64_AG 24
+#endif
+// fp64 k > 64 on gram_plain (DPP-broadcast signal pairs, a ring of PD row buffers)
+#ifndef QMFX_F64_PLAIN
+#define QMFX_F64_PLAIN 1
+#endif
+#ifndef QMFX_F64_PD
+#define QMFX_F64_PD 2
+#endif
+// VOL: volatile, so the MFMAs keep their program order against the other volatile statements
+// of the step (gram_f64_pinned places the gathers and the rhs FMAs between them that way)
+template <bool AG, bool VOL = false>
+__device__ __forceinline__ void mfma_f64_pinned(f64x4& c, double x, double y) {
+  if constexpr (AG && VOL)
+    asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
+  else if constexpr (AG)
+    asm("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
+  else if constexpr (VOL)
+    asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c) : "v"(x), "v"(y));
+  else
+    asm("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c) : "v"(x), "v"(y));
+}
+template <int i, int NTT>
+__device__ __forceinline__ void pin_tiles(f64x4 (&acc)[NTT]) {
+  if constexpr (i < NTT) {
+    if constexpr (i < QMFX_F64_AG)
+      asm volatile("" : "+a"(acc[i]));
+    else
+      asm volatile("" : "+v"(acc[i]));
+    pin_tiles<i + 1, NTT>(acc);
+  }
+}
+template <int NTT>
+__device__ __forceinline__ void gram_asm_drain(f64x4 (&acc)[NTT]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  pin_tiles<0, NTT>(acc);
+}
+// MFMAs i .. E-1 of one 4-signal step (E = NTT: the whole step), tile order (I, J ≤ I)
+template <int i, int NTT, int NT, int E = NTT, bool VOL = false>
+__device__ __forceinline__ void gram_step_pinned(f64x4 (&acc)[NTT], const double (&yv)[NT],
+                                                 const double (&wy)[NT]) {
+  if constexpr (i < E) {
+    constexpr int I = tile_row(i), J = i - I * (I + 1) / 2;
+    mfma_f64_pinned<(i < QMFX_F64_AG), VOL>(acc[i], yv[I], wy[J]);
+    gram_step_pinned<i + 1, NTT, NT, E, VOL>(acc, yv, wy);
+  }
+}
+
 // Direct-row Gram without the split (fp64, and fp32 at k ≤ 80): one 16x16x4 MFMA per tile
 // per 4 signals, straight from the gathered rows.  Signals come in chunks of 64: lane (l, g)
 // holds the (column, value) of signal 64c + g·S + l, where S = the chunk's step count (16;
@@ -202,7 +262,7 @@ template <typename T, int NT>
 constexpr int plain_depth() {
   // (fp64 k > 64 keeps its own one-step loop: gram_plain's ring spills 546 VGPRs there even
   // with VGPR-form accumulators)
-  return (sizeof(T) == 8 && NT > 4) ? 2 : 4;
+  return (sizeof(T) == 8 && NT > 4) ? QMFX_F64_PD : 4;
 }
 template <int J>
 __device__ __forceinline__ int row_bcast(int v) {
@@ -226,6 +286,7 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
                                            T (&bpart)[NT], double& csum, int lane) {
   using M = Mfma<T>;
   constexpr int KP = 16 * NT;
+  constexpr bool ASM = QMFX_F64_ASM && sizeof(T) == 8 && NT * (NT + 1) / 2 > 21;
   static_assert(16 % PD == 0, "the ring must tile a chunk");
   const int cl = lane & 15;
   const int g = lane >> 4;
@@ -283,12 +344,16 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
 #pragma unroll
     for (int q = 0; q < NT; ++q) asm volatile("" : "+v"(bpart[q]));
     asm volatile("" : "+v"(csum));
+    if constexpr (ASM) {
+      gram_step_pinned<0, NT * (NT + 1) / 2, NT>(acc, yb[b], wy);
+    } else {
 #pragma unroll
-    for (int I = 0; I < NT; ++I) {
+      for (int I = 0; I < NT; ++I) {
 #pragma unroll
-      for (int J2 = 0; J2 <= I; ++J2) {
-        const int t = tile_index(I, J2);
-        acc[t] = M::mma(yb[b][I], wy[J2], acc[t]);
+        for (int J2 = 0; J2 <= I; ++J2) {
+          const int t = tile_index(I, J2);
+          acc[t] = M::mma(yb[b][I], wy[J2], acc[t]);
+        }
       }
     }
   };
@@ -342,6 +407,138 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
     }(std::make_integer_sequence<int, PD>{});
   }
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (ASM) gram_asm_drain<NT * (NT + 1) / 2>(acc);
+}
+
+// fp64 k = 112 / 128 Gram with pinned accumulators and a hand-ordered step (QMFX_F64_ORDER).
+// Same signal layout as gram_plain (lane (l, g) holds signal 64c + g·S + l; step j's signal of
+// group g is DPP-broadcast from lane j of the row), two row buffers, the next step's rows
+// gathered one step ahead.  The step's MFMAs are volatile asm, and the other volatile
+// statements sit between them in program order: after block rows 0-1 the next step's gather
+// (its (column, value) pin, then the DPP broadcast, address and loads, which depend on the
+// pin), and after block row q the rhs FMA of y[q] (through a pin on y[q]).  So only w·y and
+// the first MFMAs wait at the step boundary; the rest issues while an MFMA holds the pipe.
+// (gram_plain's scheduler put every VALU and load of the step in front of its first MFMA.)
+#ifndef QMFX_F64_ORDER
+#define QMFX_F64_ORDER 0
+#endif
+#ifndef QMFX_F64_VOL
+#define QMFX_F64_VOL 1
+#endif
+#ifndef QMFX_F64_BPIN
+#define QMFX_F64_BPIN 1
+#endif
+#ifndef QMFX_F64_ISSUE_ROW
+#define QMFX_F64_ISSUE_ROW 2
+#endif
+template <int R, int NT>
+__device__ __forceinline__ void gram_rows_pinned(f64x4 (&acc)[NT * (NT + 1) / 2], const double (&y)[NT],
+                                                 const double (&wy)[NT]) {
+  gram_step_pinned<R * (R + 1) / 2, NT * (NT + 1) / 2, NT, (R + 1) * (R + 2) / 2, (bool)QMFX_F64_VOL>(acc, y, wy);
+}
+template <int NT>
+__device__ __forceinline__ void gram_f64_pinned(const SolveArgs<double>& a, int64_t beg, int n,
+                                                f64x4 (&acc)[NT * (NT + 1) / 2],
+                                                double (&bpart)[NT], double& csum, int lane) {
+  constexpr int KP = 16 * NT;
+  constexpr int NTT = NT * (NT + 1) / 2;
+  const int cl = lane & 15;
+  const int g = lane >> 4;
+  if (n <= 0) return;
+  const int nfull = n >> 6;
+  auto steps_of = [&](int c) {  // 16, the partial chunk's ⌈rest/4⌉, 0 past the end
+    const int rest = n - 64 * c;
+    return rest >= 64 ? 16 : (rest > 0 ? (rest + 3) >> 2 : 0);
+  };
+  auto load_chunk = [&](int c, int& cr, double& vr) {
+    const int S = steps_of(c);
+    const int e = 64 * c + g * S + cl;
+    const int64_t src = beg + ((cl < S && e < n) ? e : 0);
+    cr = a.col[src];
+    vr = a.val[src];
+  };
+  double yb[2][NT], wb[2], cwb[2];
+  auto gather = [&](bool ok, int cj, double vj, int b) {
+    const int col = ok ? cj : a.zrow;
+    const double v = ok ? vj : 0.0;
+    wb[b] = a.alpha * v;
+    cwb[b] = ok ? 1.0 + a.alpha * v : 0.0;
+    const double* yrow = a.Y + (uint64_t)(uint32_t)col * KP + cl;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) yb[b][q] = yrow[16 * q];
+  };
+  auto issue = [&](auto Jc, int S, int base, int cr, double vr, int b) {
+    constexpr int J = decltype(Jc)::value;
+    int crx = cr;
+    double vrx = vr;
+    asm volatile("" : "+v"(crx), "+v"(vrx));
+    gather(J < S && base + J < n, row_bcast<J>(crx), row_bcast<J>(vrx), b);
+  };
+  // one step from buffer b; `next` gathers the following step into the other buffer
+  auto step = [&](int b, auto&& next) {
+    __builtin_amdgcn_sched_barrier(0);
+    const double w = wb[b], cw = cwb[b];
+    double wy[NT];
+    double (&y)[NT] = yb[b];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) wy[q] = w * y[q];
+    [&]<int... R>(std::integer_sequence<int, R...>) {
+      auto row = [&](auto Rc) {
+        constexpr int r = decltype(Rc)::value;
+        gram_rows_pinned<r, NT>(acc, y, wy);
+        if constexpr (r + 1 == QMFX_F64_ISSUE_ROW) next();
+#if QMFX_F64_BPIN
+        double yq = y[r];
+        asm volatile("" : "+v"(yq));
+        bpart[r] += cw * yq;
+#else
+        bpart[r] += cw * y[r];
+#endif
+      };
+      (row(std::integral_constant<int, R>{}), ...);
+    }(std::make_integer_sequence<int, NT>{});
+    csum += cw;
+  };
+  int cr, crn;
+  double vr, vrn;
+  load_chunk(0, cr, vr);
+  load_chunk(1, crn, vrn);
+  {
+    const int S0 = steps_of(0);
+    issue(std::integral_constant<int, 0>{}, S0, g * S0, cr, vr, 0);
+  }
+  for (int c = 0; c < nfull; ++c) {
+    const int base = 64 * c + 16 * g;
+    const int Sn = steps_of(c + 1);
+    const int basen = 64 * (c + 1) + g * Sn;
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      auto one = [&](auto Jc) {
+        constexpr int j = decltype(Jc)::value;
+        step(j & 1, [&] {
+          if constexpr (j + 1 < 16)
+            issue(std::integral_constant<int, j + 1>{}, 16, base, cr, vr, (j + 1) & 1);
+          else
+            issue(std::integral_constant<int, 0>{}, Sn, basen, crn, vrn, 0);
+        });
+      };
+      (one(std::integral_constant<int, J>{}), ...);
+    }(std::make_integer_sequence<int, 16>{});
+    cr = crn;
+    vr = vrn;
+    load_chunk(c + 2, crn, vrn);
+  }
+  // the partial chunk (its step 0 already in buffer 0): two steps per iteration
+  const int St = steps_of(nfull);
+  const int baset = 64 * nfull + g * St;
+  auto gather_t = [&](int j, int b) {
+    const int src = (g << 4) + (j & 15);
+    gather(j < St && baset + j < n, __shfl(cr, src, 64), __shfl(vr, src, 64), b);
+  };
+  for (int j = 0; j < St; j += 2) {
+    step(0, [&] { gather_t(j + 1, 1); });
+    if (j + 1 < St) step(1, [&] { gather_t(j + 2, 0); });
+  }
+  gram_asm_drain<NTT>(acc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -447,12 +644,15 @@ void wals_direct_kernel(SolveArgs<T> a) {
     }
     if constexpr (Perm<NT>::template split<T>) {
       gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
-    } else if constexpr (sizeof(T) == 8 && NT > 4) {
+    } else if constexpr (sizeof(T) == 8 && NT > 4 && (!QMFX_F64_PLAIN || MODE == 1)) {
       // fp64 k > 64 (one wave, accumulators across the whole register file): the ring of
       // gram_plain costs more spills than its deeper prefetch gains; one step ahead
       // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
       // so they contribute exactly nothing without per-value selects (only Σc needs the
       // validity)
+      // (the split-K segment instance keeps the builtin: pinned, its zero-initialised tiles
+      // and the partial-image stores spilled 208 VGPRs)
+      constexpr bool ASM = QMFX_F64_ASM && NTT > 21 && MODE != 1;
       for (int64_t base = beg; base < end; base += 64) {
         const int nst = (int)(end - base < 64 ? end - base : 64);
         const int cr = lane < nst ? a.col[base + lane] : a.zrow;
@@ -485,18 +685,29 @@ void wals_direct_kernel(SolveArgs<T> a) {
 #pragma unroll
           for (int q = 0; q < NT; ++q) bpart[q] += cw * yv[q];
           csum += (double)cw;
+          if constexpr (ASM) {
+            T wy[NT];
 #pragma unroll
-          for (int I = 0; I < NT; ++I) {
+            for (int q = 0; q < NT; ++q) wy[q] = w * yv[q];
+            gram_step_pinned<0, NTT, NT>(acc, yv, wy);
+          } else {
 #pragma unroll
-            for (int J = 0; J <= I; ++J) {
-              const int t = tile_index(I, J);
-              acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+            for (int I = 0; I < NT; ++I) {
+#pragma unroll
+              for (int J = 0; J <= I; ++J) {
+                const int t = tile_index(I, J);
+                acc[t] = M::mma(yv[I], w * yv[J], acc[t]);
+              }
             }
           }
         }
       }
+      if constexpr (ASM) gram_asm_drain<NTT>(acc);
     } else {
-      gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
+      if constexpr (sizeof(T) == 8 && NT * (NT + 1) / 2 > 21 && QMFX_F64_ASM && QMFX_F64_ORDER)
+        gram_f64_pinned<NT>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
+      else
+        gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
     }
 #pragma unroll
     for (int q = 0; q < NT; ++q) {

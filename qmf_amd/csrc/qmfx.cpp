@@ -163,6 +163,7 @@ struct qmfx_ctx {
   int fault_comm_rank = -1;
   int64_t fault_comm_after = 0, comm_pieces_done = 0;
   bool whitened_enabled = true;  // QMFX_NO_WHITEN=1 forces the direct kernel for every row
+  int wb_k64_ntn = 0;            // QMFX_WB_K64_NTN: largest whitened bucket at k = 64 (0: default)
   // the half-epoch in progress (qmfx_wals_half's phases)
   struct HalfStateT {
     int side = 0;
@@ -309,9 +310,13 @@ bool use_big_rows(const qmfx_ctx* c) { return c->nt > 8; }
 // direct).
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
+  if (c->nt == 4 && c->wb_k64_ntn > 0) return c->wb_k64_ntn;
   if (c->prec == 32) {
     if (c->nt == 8 || c->nt == 16) return 8;
     if (c->nt > 8) return 0;  // fp32 k = 144..240: every row on the big k×k kernel
+    // k = 64: n ≤ 48 (a 48×48 factorization instead of 64×64; C2 same-box A/B 10.0 → 9.1
+    // ms/epoch, round 5; the fp64 register-resident kernel measured slower there)
+    if (c->nt == 4) return 3;
     return std::min(c->nt / 2, 4);
   }
   if (c->nt == 8 || c->nt == 16) return 5;
@@ -568,6 +573,7 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->kp = 16 * nt;
   c->esz = precision == 32 ? 4 : 8;
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
+  if (const char* w = std::getenv("QMFX_WB_K64_NTN")) c->wb_k64_ntn = std::min(std::max(std::atoi(w), 1), 3);
   if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK")) {
     c->fault_comm_rank = std::atoi(f);
     if (const char* a = std::strchr(f, ':')) c->fault_comm_after = std::atoll(a + 1);

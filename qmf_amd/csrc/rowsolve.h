@@ -5,6 +5,12 @@
 namespace qmfx {
 
 __host__ __device__ constexpr int tile_index(int I, int J) { return I * (I + 1) / 2 + J; }
+// the block row I of lower tile t (tile_index(I, J) = t)
+__host__ __device__ constexpr int tile_row(int t) {
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  return I;
+}
 
 // Square root / reciprocal inside the factorizations.  fp32: hardware v_sqrt_f32 /
 // v_rcp_f32 (1 ulp; the IEEE-exact expansions cost ~27 instructions each, on the critical

@@ -1136,7 +1136,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
           if constexpr (NTK >= 4) QMFX_WBS(2);
           return hipErrorInvalidValue;
         case 3:
-          if constexpr (NTK >= 6) QMFX_WBS(3);
+          if constexpr (NTK >= 4) QMFX_WBS(3);
           return hipErrorInvalidValue;
         case 4:
           if constexpr (NTK >= 8) QMFX_WBS(4);
@@ -1172,7 +1172,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
     if constexpr (NTK >= 4) QMFX_WB(2);
     else return hipErrorInvalidValue;
   } else if (ntn == 3) {
-    if constexpr (NTK >= 6) QMFX_WB(3);
+    if constexpr (NTK >= 4) QMFX_WB(3);
     else return hipErrorInvalidValue;
   } else if (ntn == 4) {
     if constexpr (NTK >= 8) QMFX_WB(4);
