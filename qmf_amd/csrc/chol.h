@@ -9,18 +9,11 @@
 namespace qmfx {
 
 // ---------------------------------------------------------------------------------------
-// Register-tile Cholesky + solve, shared by both row kernels (one wave64 per system).
+// Register-tile LDLᵀ factorization + solves of one SPD system per wave64, shared by the
+// direct and the whitened row kernels (the method: chol_solve's comment below).
 //   In:  acc = lower 16×16 tiles of an SPD matrix of size 16·NT (diagonal tiles full);
 //        S.bw = right-hand side (written and synchronised by the caller).
-//   Out: S.xs = solution; S.bw = L⁻¹ b.  `bad` set on a non-positive pivot.
-// Right-looking over 16-column panels.  A panel is factored with its rows spread over the
-// lanes: per column one broadcast (readlane) of the diagonal block's column, issued
-// before the pivot is known, and unconditional FMAs (rows above the pivot only touch
-// their dead upper part); the forward solve rides along as one more register per row.
-// The trailing update A(I,J) −= L(I,p)L(J,p)ᵀ is 4 MFMAs per tile with operands staged
-// through LDS; off-diagonal L tiles return to the registers.  The diagonal L blocks go to
-// LDS transposed and column-scaled, Lt[q][c] = L[c][q]/L[q][q] (q < c, 0 elsewhere), so
-// the backward substitution is one readlane + one FMA per column.
+//   Out: S.xs = solution.  `bad` set on a non-positive pivot.
 // ---------------------------------------------------------------------------------------
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -202,7 +195,8 @@ __device__ __forceinline__ void slot_column(const double (&dg)[16], double invv,
 //   The trailing update A(I,J) −= U(I,p) D⁻¹ U(J,p)ᵀ is 4 MFMAs per tile with operands from
 //   the LDS panel (the J operand scaled by 1/d of its column); the diagonal blocks go to LDS
 //   transposed and scaled, Lt[q][c] = U[c][q]/d_q (c > q), for the backward substitution
-//   (one readlane + one FMA per column).
+//   (QMFX_BW_DPP, the default: one v_fmac_dpp row_newbcast per column instead of a readlane
+//   + an FMA).
 // In: acc = lower 16×16 tiles of the SPD matrix; S.bw = right-hand side.  Out: S.xs = x.
 // `bad` is set on a pivot that is not positive (or not finite).
 // ---------------------------------------------------------------------------------------

@@ -208,16 +208,10 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_F64_PD
 #define QMFX_F64_PD 2
 #endif
-// VOL: volatile, so the MFMAs keep their program order against the other volatile statements
-// of the step (gram_f64_pinned places the gathers and the rhs FMAs between them that way)
-template <bool AG, bool VOL = false>
+template <bool AG>
 __device__ __forceinline__ void mfma_f64_pinned(f64x4& c, double x, double y) {
-  if constexpr (AG && VOL)
-    asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
-  else if constexpr (AG)
+  if constexpr (AG)
     asm("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
-  else if constexpr (VOL)
-    asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c) : "v"(x), "v"(y));
   else
     asm("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c) : "v"(x), "v"(y));
 }
@@ -236,14 +230,14 @@ __device__ __forceinline__ void gram_asm_drain(f64x4 (&acc)[NTT]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   pin_tiles<0, NTT>(acc);
 }
-// MFMAs i .. E-1 of one 4-signal step (E = NTT: the whole step), tile order (I, J ≤ I)
-template <int i, int NTT, int NT, int E = NTT, bool VOL = false>
+// the MFMAs of one 4-signal step, tile order (I, J ≤ I)
+template <int i, int NTT, int NT>
 __device__ __forceinline__ void gram_step_pinned(f64x4 (&acc)[NTT], const double (&yv)[NT],
                                                  const double (&wy)[NT]) {
-  if constexpr (i < E) {
+  if constexpr (i < NTT) {
     constexpr int I = tile_row(i), J = i - I * (I + 1) / 2;
-    mfma_f64_pinned<(i < QMFX_F64_AG), VOL>(acc[i], yv[I], wy[J]);
-    gram_step_pinned<i + 1, NTT, NT, E, VOL>(acc, yv, wy);
+    mfma_f64_pinned<(i < QMFX_F64_AG)>(acc[i], yv[I], wy[J]);
+    gram_step_pinned<i + 1, NTT, NT>(acc, yv, wy);
   }
 }
 
@@ -410,137 +404,6 @@ __device__ __forceinline__ void gram_plain(const SolveArgs<T>& a, int64_t beg, i
   if constexpr (ASM) gram_asm_drain<NT * (NT + 1) / 2>(acc);
 }
 
-// fp64 k = 112 / 128 Gram with pinned accumulators and a hand-ordered step (QMFX_F64_ORDER).
-// Same signal layout as gram_plain (lane (l, g) holds signal 64c + g·S + l; step j's signal of
-// group g is DPP-broadcast from lane j of the row), two row buffers, the next step's rows
-// gathered one step ahead.  The step's MFMAs are volatile asm, and the other volatile
-// statements sit between them in program order: after block rows 0-1 the next step's gather
-// (its (column, value) pin, then the DPP broadcast, address and loads, which depend on the
-// pin), and after block row q the rhs FMA of y[q] (through a pin on y[q]).  So only w·y and
-// the first MFMAs wait at the step boundary; the rest issues while an MFMA holds the pipe.
-// (gram_plain's scheduler put every VALU and load of the step in front of its first MFMA.)
-#ifndef QMFX_F64_ORDER
-#define QMFX_F64_ORDER 0
-#endif
-#ifndef QMFX_F64_VOL
-#define QMFX_F64_VOL 1
-#endif
-#ifndef QMFX_F64_BPIN
-#define QMFX_F64_BPIN 1
-#endif
-#ifndef QMFX_F64_ISSUE_ROW
-#define QMFX_F64_ISSUE_ROW 2
-#endif
-template <int R, int NT>
-__device__ __forceinline__ void gram_rows_pinned(f64x4 (&acc)[NT * (NT + 1) / 2], const double (&y)[NT],
-                                                 const double (&wy)[NT]) {
-  gram_step_pinned<R * (R + 1) / 2, NT * (NT + 1) / 2, NT, (R + 1) * (R + 2) / 2, (bool)QMFX_F64_VOL>(acc, y, wy);
-}
-template <int NT>
-__device__ __forceinline__ void gram_f64_pinned(const SolveArgs<double>& a, int64_t beg, int n,
-                                                f64x4 (&acc)[NT * (NT + 1) / 2],
-                                                double (&bpart)[NT], double& csum, int lane) {
-  constexpr int KP = 16 * NT;
-  constexpr int NTT = NT * (NT + 1) / 2;
-  const int cl = lane & 15;
-  const int g = lane >> 4;
-  if (n <= 0) return;
-  const int nfull = n >> 6;
-  auto steps_of = [&](int c) {  // 16, the partial chunk's ⌈rest/4⌉, 0 past the end
-    const int rest = n - 64 * c;
-    return rest >= 64 ? 16 : (rest > 0 ? (rest + 3) >> 2 : 0);
-  };
-  auto load_chunk = [&](int c, int& cr, double& vr) {
-    const int S = steps_of(c);
-    const int e = 64 * c + g * S + cl;
-    const int64_t src = beg + ((cl < S && e < n) ? e : 0);
-    cr = a.col[src];
-    vr = a.val[src];
-  };
-  double yb[2][NT], wb[2], cwb[2];
-  auto gather = [&](bool ok, int cj, double vj, int b) {
-    const int col = ok ? cj : a.zrow;
-    const double v = ok ? vj : 0.0;
-    wb[b] = a.alpha * v;
-    cwb[b] = ok ? 1.0 + a.alpha * v : 0.0;
-    const double* yrow = a.Y + (uint64_t)(uint32_t)col * KP + cl;
-#pragma unroll
-    for (int q = 0; q < NT; ++q) yb[b][q] = yrow[16 * q];
-  };
-  auto issue = [&](auto Jc, int S, int base, int cr, double vr, int b) {
-    constexpr int J = decltype(Jc)::value;
-    int crx = cr;
-    double vrx = vr;
-    asm volatile("" : "+v"(crx), "+v"(vrx));
-    gather(J < S && base + J < n, row_bcast<J>(crx), row_bcast<J>(vrx), b);
-  };
-  // one step from buffer b; `next` gathers the following step into the other buffer
-  auto step = [&](int b, auto&& next) {
-    __builtin_amdgcn_sched_barrier(0);
-    const double w = wb[b], cw = cwb[b];
-    double wy[NT];
-    double (&y)[NT] = yb[b];
-#pragma unroll
-    for (int q = 0; q < NT; ++q) wy[q] = w * y[q];
-    [&]<int... R>(std::integer_sequence<int, R...>) {
-      auto row = [&](auto Rc) {
-        constexpr int r = decltype(Rc)::value;
-        gram_rows_pinned<r, NT>(acc, y, wy);
-        if constexpr (r + 1 == QMFX_F64_ISSUE_ROW) next();
-#if QMFX_F64_BPIN
-        double yq = y[r];
-        asm volatile("" : "+v"(yq));
-        bpart[r] += cw * yq;
-#else
-        bpart[r] += cw * y[r];
-#endif
-      };
-      (row(std::integral_constant<int, R>{}), ...);
-    }(std::make_integer_sequence<int, NT>{});
-    csum += cw;
-  };
-  int cr, crn;
-  double vr, vrn;
-  load_chunk(0, cr, vr);
-  load_chunk(1, crn, vrn);
-  {
-    const int S0 = steps_of(0);
-    issue(std::integral_constant<int, 0>{}, S0, g * S0, cr, vr, 0);
-  }
-  for (int c = 0; c < nfull; ++c) {
-    const int base = 64 * c + 16 * g;
-    const int Sn = steps_of(c + 1);
-    const int basen = 64 * (c + 1) + g * Sn;
-    [&]<int... J>(std::integer_sequence<int, J...>) {
-      auto one = [&](auto Jc) {
-        constexpr int j = decltype(Jc)::value;
-        step(j & 1, [&] {
-          if constexpr (j + 1 < 16)
-            issue(std::integral_constant<int, j + 1>{}, 16, base, cr, vr, (j + 1) & 1);
-          else
-            issue(std::integral_constant<int, 0>{}, Sn, basen, crn, vrn, 0);
-        });
-      };
-      (one(std::integral_constant<int, J>{}), ...);
-    }(std::make_integer_sequence<int, 16>{});
-    cr = crn;
-    vr = vrn;
-    load_chunk(c + 2, crn, vrn);
-  }
-  // the partial chunk (its step 0 already in buffer 0): two steps per iteration
-  const int St = steps_of(nfull);
-  const int baset = 64 * nfull + g * St;
-  auto gather_t = [&](int j, int b) {
-    const int src = (g << 4) + (j & 15);
-    gather(j < St && baset + j < n, __shfl(cr, src, 64), __shfl(vr, src, 64), b);
-  };
-  for (int j = 0; j < St; j += 2) {
-    step(0, [&] { gather_t(j + 1, 1); });
-    if (j + 1 < St) step(1, [&] { gather_t(j + 2, 0); });
-  }
-  gram_asm_drain<NTT>(acc);
-}
-
 // ---------------------------------------------------------------------------------------
 // Direct row kernel: one wave64 per row (slot order heaviest-first).  Gram
 // A = G + λI + Σ w y yᵀ accumulated into the lower tiles held in registers, starting from
@@ -704,10 +567,7 @@ void wals_direct_kernel(SolveArgs<T> a) {
       }
       if constexpr (ASM) gram_asm_drain<NTT>(acc);
     } else {
-      if constexpr (sizeof(T) == 8 && NT * (NT + 1) / 2 > 21 && QMFX_F64_ASM && QMFX_F64_ORDER)
-        gram_f64_pinned<NT>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
-      else
-        gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
+      gram_plain<T, NT, plain_depth<T, NT>()>(a, beg, (int)(end - beg), acc, bpart, csum, lane);
     }
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
