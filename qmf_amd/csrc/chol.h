@@ -125,11 +125,6 @@ __device__ __forceinline__ double pivot_rcp(double d) {
   return __builtin_fma(r, e, r);
 }
 
-// QMFX_DG_SB: one scheduling region per column (0: the next column's pivot chain may issue
-// among this column's DPP FMAs once its diagonal entry is updated)
-#ifndef QMFX_DG_SB
-#define QMFX_DG_SB 1
-#endif
 // Column C of an fp64 panel in the replicated-diagonal layout (chol_solve below): the pivot
 // d = U[C][C] and z_C = b_C broadcast from lane C of every 16-lane row, l = U[q][C]/d, the
 // right-hand sides' update, and the trailing columns m > C of the diagonal block and of the
@@ -162,7 +157,7 @@ __device__ __forceinline__ void dg_column(double (&dg)[16], double& bdg, double 
     };
     (upd(std::integral_constant<int, Ms>{}), ...);
   }(std::make_integer_sequence<int, 16>{});
-  if constexpr (QMFX_DG_SB) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
 }
 // Column C for a further slot of rows, after the diagonal block is factored: its final
 // column C is what column C broadcast, and lane C holds 1/d_C and z_C.
@@ -180,7 +175,7 @@ __device__ __forceinline__ void slot_column(const double (&dg)[16], double invv,
     };
     (upd(std::integral_constant<int, Ms>{}), ...);
   }(std::make_integer_sequence<int, 16>{});
-  if constexpr (QMFX_DG_SB) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // ---------------------------------------------------------------------------------------

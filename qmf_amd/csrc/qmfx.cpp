@@ -573,7 +573,7 @@ int qmfx_create(qmfx_ctx** out, int device, int precision, int nfactors) {
   c->kp = 16 * nt;
   c->esz = precision == 32 ? 4 : 8;
   if (const char* nw = std::getenv("QMFX_NO_WHITEN")) c->whitened_enabled = std::atoi(nw) == 0;
-  if (const char* w = std::getenv("QMFX_WB_K64_NTN")) c->wb_k64_ntn = std::min(std::max(std::atoi(w), 1), 3);
+  if (const char* w = std::getenv("QMFX_WB_K64_NTN")) c->wb_k64_ntn = std::min(std::max(std::atoi(w), 1), 4);
   if (const char* f = std::getenv("QMFX_FAULT_COMM_RANK")) {
     c->fault_comm_rank = std::atoi(f);
     if (const char* a = std::strchr(f, ':')) c->fault_comm_after = std::atoll(a + 1);

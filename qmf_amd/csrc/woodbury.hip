@@ -1139,7 +1139,7 @@ static hipError_t launch_woodbury_ntk(const SolveArgs<T>& a, int ntn, hipStream_
           if constexpr (NTK >= 4) QMFX_WBS(3);
           return hipErrorInvalidValue;
         case 4:
-          if constexpr (NTK >= 8) QMFX_WBS(4);
+          if constexpr (NTK >= 4) QMFX_WBS(4);
           return hipErrorInvalidValue;
         // n = 65..128 (two signals per lane): fp32 k = 128 and 256
         case 5:
