@@ -35,9 +35,6 @@
 #ifndef QMFX_BIG_SIG64
 #define QMFX_BIG_SIG64 16
 #endif
-#ifndef QMFX_BIG_PAIR64
-#define QMFX_BIG_PAIR64 0
-#endif
 #ifndef QMFX_BIG_SPLIT
 #define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
 #endif
@@ -56,11 +53,9 @@ struct BigCfg {
   // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
   // planes once per stage for both rows
   static constexpr bool SPLIT = sizeof(T) == 4 && NT == 2 * NW && QMFX_BIG_SPLIT;
-  // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles): the split Gram,
-  // and fp64 k = 256 with the lean pair steps below (QMFX_BIG_PAIR64; round 4's pair map
-  // held every fragment of the step in registers and spilled 248 VGPRs)
-  static constexpr bool PAIR64 = sizeof(T) == 8 && NT == 2 * NW && QMFX_BIG_PAIR64;
-  static constexpr bool PAIR = SPLIT || PAIR64;
+  // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles) for the split Gram
+  // (fp64 k = 256 on this map spilled 248 VGPRs against 84: round 4, tools/exp)
+  static constexpr bool PAIR = SPLIT;
   static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
@@ -77,19 +72,7 @@ struct BigCfg {
 // tile s of wave W: round-robin t = W + NW·s, or (split map) rows W and NT−1−W
 template <typename C>
 __host__ __device__ constexpr void big_tile(int W, int s, int& I, int& J) {
-  if constexpr (C::PAIR64) {
-    // wave W: row B = NT−1−W in slots 0..B (slot J = tile (B, J)), row A = W in slots
-    // NT−A..NT (slot NT − J = tile (A, J)): the same compile-time slot for a given J on every
-    // wave, so one loop body serves all waves (per-wave specialisations spilled 187 VGPRs)
-    constexpr int NT = C::KP / 16;
-    if (s <= NT - 1 - W) {
-      I = NT - 1 - W;
-      J = s;
-    } else {
-      I = W;
-      J = NT - s;
-    }
-  } else if constexpr (C::PAIR) {
+  if constexpr (C::PAIR) {
     constexpr int NT = C::KP / 16;
     if (s <= W) {
       I = W;
@@ -252,57 +235,6 @@ __device__ __forceinline__ void big_trailing(typename Mfma<T>::acc_t* acc, const
     if (I >= 0 && J > p) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[s] = M::mma(-fr[I][q], fr[J][q], acc[s]);
-    }
-  }
-}
-
-// Pair-map Gram step (fp64 k = 256; wave W owns block rows A = W and B = NT−1−W, slots as in
-// big_tile): per 4-signal step the two A-operand fragments and each B-operand fragment J ≤ B
-// are read from LDS once and w·y[J] feeds both rows' tiles — NT − W + 2 reads for NT + 1
-// MFMAs (two reads per MFMA on the round-robin map, whose fragments do not fit the registers
-// at k = 256).  The row bounds are wave-uniform branches.
-template <typename T, int NT>
-__device__ __forceinline__ void big_pair_step(typename Mfma<T>::acc_t* acc, const T* yk, T wk,
-                                              int A, int B) {
-  using M = Mfma<T>;
-  const T ya = yk[16 * A], yb = yk[16 * B];
-#pragma unroll
-  for (int J = 0; J < NT; ++J) {
-    if (J <= B) {
-      const T wj = wk * yk[16 * J];
-      acc[J] = M::mma(yb, wj, acc[J]);                      // tile (B, J)
-      if (J <= A) acc[NT - J] = M::mma(ya, wj, acc[NT - J]);  // tile (A, J)
-    }
-  }
-}
-
-// Pair-map trailing update of panel p: the panel fragments of blocks A and B once, then each
-// block J (p < J ≤ B) once for both rows' tiles.
-template <typename T, int NT>
-__device__ __forceinline__ void big_pair_trailing(typename Mfma<T>::acc_t* acc, const T* panel,
-                                                  int p, int cl, int kk, int A, int B) {
-  using C = BigCfg<T, NT>;
-  using M = Mfma<T>;
-  if (B <= p) return;
-  auto rd = [&](int X, T (&f)[4]) {
-    const T* src = panel + (16 * (X - p) + cl) * C::PLD + kk;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) f[q] = src[4 * q];
-  };
-  T fa[4], fb[4];
-  rd(A > p ? A : B, fa);
-  rd(B, fb);
-#pragma unroll
-  for (int J = 1; J < NT; ++J) {
-    if (J > p && J <= B) {
-      T fj[4];
-      rd(J, fj);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[J] = M::mma(-fb[q], fj[q], acc[J]);
-      if (J <= A) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[NT - J] = M::mma(-fa[q], fj[q], acc[NT - J]);
-      }
     }
   }
 }
@@ -571,11 +503,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
           big_gram_step<T, NT, W>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk]);
       };
       static_assert(NW == 2 || NW == 4 || NW == 8 || NW == 16, "wave count");
-      if constexpr (C::PAIR64) {
-#pragma unroll 2
-        for (int k4 = 0; k4 < SIG; k4 += 4)
-          big_pair_step<T, NT>(acc, sg + (k4 + kk) * KP + cl, S.w[buf][k4 + kk], wv, NT - 1 - wv);
-      } else if constexpr (C::REUSE) {
+      if constexpr (C::REUSE) {
         dispatch_wave<NW>(wv, gram_stage);
       } else {
 #pragma unroll 2
@@ -656,9 +584,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
           acc[s][r] = S.panel[(16 * (TI[s] - p) + M::crow(lane, r)) * PLD + cl];
       }
     }
-    if constexpr (C::PAIR64) {
-      if (p + 1 < NT) big_pair_trailing<T, NT>(acc, S.panel, p, cl, kk, wv, NT - 1 - wv);
-    } else if constexpr (!C::REUSE) {
+    if constexpr (!C::REUSE) {
 #pragma unroll
       for (int s = 0; s < TPW; ++s) {
         if (TJ[s] > p) {
