@@ -117,12 +117,17 @@ __device__ __forceinline__ void fmac_bcast16(float& acc, float src, float m) {
 // 1/d for the LDLᵀ pivots: fp32 v_rcp_f32 (1 ulp); fp64 v_rcp_f64 + two Newton steps (an ulp
 // or so; a non-positive or NaN d leaves the result outside (0, ∞), which the caller flags)
 __device__ __forceinline__ float pivot_rcp(float d) { return __builtin_amdgcn_rcpf(d); }
+#ifndef QMFX_RCP_NEWTON
+#define QMFX_RCP_NEWTON 2
+#endif
 __device__ __forceinline__ double pivot_rcp(double d) {
   double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  return __builtin_fma(r, e, r);
+#pragma unroll
+  for (int i = 0; i < QMFX_RCP_NEWTON; ++i) {
+    const double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+  }
+  return r;
 }
 
 // Column C of an fp64 panel in the replicated-diagonal layout (chol_solve below): the pivot

@@ -310,17 +310,20 @@ bool use_big_rows(const qmfx_ctx* c) { return c->nt > 8; }
 // direct).
 int max_whitened_ntn(const qmfx_ctx* c) {
   if (!c->whitened_enabled) return 0;
-  if (c->nt == 4 && c->wb_k64_ntn > 0) return std::min(c->wb_k64_ntn, c->prec == 32 ? 4 : 3);
+  if (c->nt == 4 && c->wb_k64_ntn > 0) return std::min(c->wb_k64_ntn, 4);
   if (c->prec == 32) {
     if (c->nt == 8 || c->nt == 16) return 8;
     if (c->nt > 8) return 0;  // fp32 k = 144..240: every row on the big k×k kernel
     // k = 64: n ≤ 64 (C2 same-box A/Bs, round 5: n ≤ 32 → n ≤ 48 10.0 → 9.1 ms/epoch, → n ≤ 64
-    // 8.7 → 8.2; fp64 k = 64 stays at n ≤ 32: its register-resident kernel measured slower)
+    // 8.7 → 8.2)
     if (c->nt == 4) return 4;
     return std::min(c->nt / 2, 4);
   }
   if (c->nt == 8 || c->nt == 16) return 5;
   if (c->nt > 8) return 0;
+  // k = 64: n ≤ 48 on the streamed fp64 kernel (C2 fp64 same-box A/B, round 5: 18.5 → 17.6
+  // ms/epoch; n ≤ 64 measured no better)
+  if (c->nt == 4) return 3;
   return std::min(c->nt / 2, c->nt <= 4 ? 2 : 4);
 }
 

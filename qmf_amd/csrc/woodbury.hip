@@ -627,6 +627,11 @@ constexpr int wb64_kdepth() {
 // the rest are gathered again): the registers the n×n Cholesky leaves free at two waves per
 // SIMD (fp64 whitened rows are bound by the fabric's random-row rate, so every chunk not
 // re-gathered is 1/NTK of the second pass's bytes)
+// fp64 k = 64 whitened rows on the streamed kernel (round 5: C2 fp64 18.5 -> 17.6 ms/epoch
+// with n ≤ 48 whitened; the register-resident kernel measured slower there)
+#ifndef QMFX_WB64_K64
+#define QMFX_WB64_K64 1
+#endif
 #ifndef QMFX_WB64_KEEP2
 #define QMFX_WB64_KEEP2 6
 #endif
@@ -1201,10 +1206,10 @@ static hipError_t launch_woodbury_st64_ntk(const SolveArgs<double>& a, int ntn, 
     case 1: QMFX_WBS64(1);
     case 2: QMFX_WBS64(2);
     case 3:
-      if constexpr (NTK >= 6) QMFX_WBS64(3);
+      if constexpr (NTK >= 4) QMFX_WBS64(3);
       return hipErrorInvalidValue;
     case 4:
-      if constexpr (NTK >= 8) QMFX_WBS64(4);
+      if constexpr (NTK >= 4) QMFX_WBS64(4);
       return hipErrorInvalidValue;
     // n = 65..80 (two signals per lane) at k = 128 and 256 (n > 80 spills: direct)
     case 5:
@@ -1306,8 +1311,11 @@ hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipS
 #undef CALL
 }
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
-  // one wave up to k = 64; k = 80..128 and 256 on the streamed fp64 kernel
+  // k = 64 .. 128 and 256 on the streamed fp64 kernel; the register-resident one below
   switch (nt) {
+#if QMFX_WB64_K64
+    case 4: return launch_woodbury_st64_ntk<4>(a, ntn, s);
+#endif
     case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
     case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
     case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);

@@ -231,8 +231,8 @@ def test_row_system_matches_oracle():
     # signals (every n×n bucket up to n = 64)
     (128, 64, 30000), (128, 64, 160000), (80, 64, 160000), (112, 64, 160000), (80, 64, 30000),
     (256, 32, 160000),
-    # k = 64, ~40 signals per user: fp32 whitens n ≤ 64 (the NTN = 3 / 4 buckets, round 5),
-    # fp64 n ≤ 32
+    # k = 64, ~40 signals per user: fp32 whitens n ≤ 64 (the NTN = 3 / 4 buckets), fp64
+    # n ≤ 48 on the streamed fp64 kernel (round 5)
     (64, 32, 160000), (64, 64, 160000),
     # fp32 k = 256 / 128, ~100 signals per user: the n = 65..128 buckets (two signals per
     # lane)
@@ -255,7 +255,7 @@ def test_whitened_rows_match_direct_and_oracle(k, precision, nnz, monkeypatch):
         assert wb[4] > 0, wb
     if k == 64 and nnz == 160000:
         wb = c.row_classes(0)["whitened"]
-        assert (wb[2] > 0 and wb[3] > 0) == (precision == 32), wb
+        assert wb[2] > 0 and (wb[3] > 0) == (precision == 32), wb
     monkeypatch.setenv("QMFX_NO_WHITEN", "1")
     _, cd = make_pair(u, i, v, k, precision, seed=2)
     assert sum(cd.row_classes(0)["whitened"]) == 0
