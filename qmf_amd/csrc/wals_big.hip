@@ -17,6 +17,7 @@
 //     wave 0 finishes the block with the diagonal triangle.
 // Same results contract as the single-wave kernels: status[row] = 1 on a non-positive pivot.
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 
@@ -38,6 +39,12 @@
 #ifndef QMFX_BIG_SPLIT
 #define QMFX_BIG_SPLIT 1  // fp32 k = 256: the split-bf16 Gram from LDS (QMFX_BIG_SPLIT=0: f32 MFMA)
 #endif
+#ifndef QMFX_BIG_STREAM
+#define QMFX_BIG_STREAM 1  // fp64: per-wave streamed Gram (0: the LDS-staged Gram)
+#endif
+#ifndef QMFX_BIG_PAIR64
+#define QMFX_BIG_PAIR64 1  // fp64 k = 256: row-pair tile map (0: round-robin)
+#endif
 
 namespace qmfx {
 
@@ -53,9 +60,11 @@ struct BigCfg {
   // and wave W owns block rows W and NT−1−W (NT + 1 tiles), reading each column block's
   // planes once per stage for both rows
   static constexpr bool SPLIT = sizeof(T) == 4 && NT == 2 * NW && QMFX_BIG_SPLIT;
-  // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles) for the split Gram
-  // (fp64 k = 256 on this map spilled 248 VGPRs against 84: round 4, tools/exp)
-  static constexpr bool PAIR = SPLIT;
+  // fp64: every wave gathers its own operand fragments of the row's signals (big_gram_stream),
+  // with no LDS staging and no barrier in the Gram
+  static constexpr bool STREAM = sizeof(T) == 8 && QMFX_BIG_STREAM;
+  // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles)
+  static constexpr bool PAIR = SPLIT || (STREAM && NT == 2 * NW && QMFX_BIG_PAIR64);
   static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
@@ -99,7 +108,7 @@ struct BigShared {
   using C = BigCfg<T, NT>;
   // the Gram staging and the Cholesky panels are never live together
   union {
-    T stage[2][C::SIG * C::KP];
+    T stage[2][C::STREAM ? 1 : C::SIG * C::KP];
     uint16_t planes[2][3][C::SPLIT ? C::KP * C::SPAD : 1];  // split Gram: bf16 hi/mid/lo, [column][signal]
     float bred[8][C::KP];                    // split Gram: per-wave b partials (after the Gram)
     struct {
@@ -239,6 +248,159 @@ __device__ __forceinline__ void big_trailing(typename Mfma<T>::acc_t* acc, const
   }
 }
 
+// Streamed Gram (fp64): the blocks wave W needs — its tiles' block rows and columns and the
+// blocks of b it owns (big_b_owner) — as bit masks, fixed at compile time.
+template <typename C>
+__host__ __device__ constexpr int big_b_owner(int X) {
+  constexpr int NT = C::KP / 16;
+  if constexpr (C::PAIR) return X < NT - 1 - X ? X : NT - 1 - X;
+  return X % C::NW;
+}
+template <typename C, int W>
+constexpr uint32_t big_rows_mask() {
+  uint32_t m = 0;
+  for (int s = 0; s < C::TPW; ++s) {
+    int I = -1, J = -1;
+    big_tile<C>(W, s, I, J);
+    if (I >= 0) m |= 1u << I;
+  }
+  return m;
+}
+template <typename C, int W>
+constexpr uint32_t big_need_mask() {
+  uint32_t m = big_rows_mask<C, W>();
+  for (int s = 0; s < C::TPW; ++s) {
+    int I = -1, J = -1;
+    big_tile<C>(W, s, I, J);
+    if (I >= 0) m |= 1u << J;
+  }
+  for (int X = 0; X < C::KP / 16; ++X)
+    if (big_b_owner<C>(X) == W) m |= 1u << X;
+  return m;
+}
+
+// The streamed Gram's block order within a step: the wave's tile-row blocks first (their w·y
+// start the next step, so they are gathered again first), then the other blocks ascending.
+template <typename C, int W>
+constexpr int big_jorder(int q) {
+  constexpr uint32_t rows = big_rows_mask<C, W>();
+  for (int pass = 0; pass < 2; ++pass)
+    for (int X = 0; X < C::KP / 16; ++X)
+      if ((((rows >> X) & 1) != 0) == (pass == 0) && q-- == 0) return X;
+  return 0;
+}
+
+// Streamed Gram of wave W (fp64 multi-wave rows): A_tiles += Σ w y yᵀ over the row's signals
+// for the wave's own tiles, and b_X = Σ c y_X for the blocks it owns.  Step t takes signals
+// 4t..4t+3, one per 16-lane group (the MFMA's K index): lane (cl, g) gathers element
+// 16X + cl of signal 4t + g for each block X the wave needs (one 8-B load per block, the
+// same base address with an immediate offset), scales its tile-row blocks by w and issues one
+// 16x16x4 MFMA per tile.  No LDS and no barrier: every wave runs ahead on its own, the other
+// waves of the row read the same rows from L2.  (column, value) pairs are loaded CD steps
+// ahead into a ring, the rows of step t + 2 while step t's MFMAs run (2 buffers).  Loads are
+// unconditional (a clamped address past the end; the all-zero row a.zrow with w = 0 at use).
+template <typename T, int NT, int W>
+__device__ __forceinline__ void big_gram_stream(const SolveArgs<T>& a, int64_t beg, int n,
+                                                typename Mfma<T>::acc_t (&acc)[BigCfg<T, NT>::TPW],
+                                                T (&bq)[NT], int lane) {
+  using C = BigCfg<T, NT>;
+  using M = Mfma<T>;
+  constexpr int KP = C::KP, TPW = C::TPW;
+  constexpr uint32_t ROWS = big_rows_mask<C, W>();
+  constexpr uint32_t NEED = big_need_mask<C, W>();
+  // column ring: loaded CD steps ahead, used for the gather two steps ahead
+  constexpr int CD = 4;
+  const int cl = lane & 15, g = lane >> 4;
+  const int nsteps = (n + 3) >> 2;
+  if (nsteps == 0) return;
+  int cr[CD];
+  T yb[2][NT];
+  T vb[2];
+  auto ldcol = [&](int t, int& c) {
+    const int e = 4 * t + g;
+    c = a.col[beg + (e < n ? e : 0)];
+  };
+  // the row base and the value of step t (value loaded with the rows: consumed a step later)
+  auto rowbase = [&](int t, int c, int b) -> const T* {
+    const int e = 4 * t + g;
+    const bool ok = e < n;
+    const uint32_t col = ok ? (uint32_t)c : (uint32_t)a.zrow;
+    vb[b] = a.val[beg + (ok ? e : 0)];
+    return a.Y + (uint64_t)col * KP + cl;
+  };
+  auto gather = [&](int t, int c, int b) {
+    const T* yr = rowbase(t, c, b);
+#pragma unroll
+    for (int X = 0; X < NT; ++X)
+      if ((NEED >> X) & 1) yb[b][X] = yr[16 * X];
+  };
+  // step u from buffer b, and the gathers of step u + 2 into b: block J's fragment is loaded
+  // again right after the step's last MFMA that reads it (tiles (I, J) in J order), so each
+  // gather is in flight for about two steps instead of one
+  auto step = [&](int b, int tn, int cn) {
+    // (past the end: the zero row, whatever the value; it adds nothing to the tiles or b)
+    const T w = a.alpha * vb[b];
+    const T cw = T(1) + w;
+    T wy[NT];
+#pragma unroll
+    for (int X = 0; X < NT; ++X) {
+      if ((ROWS >> X) & 1) wy[X] = w * yb[b][X];
+      if (big_b_owner<C>(X) == W) bq[X] += cw * yb[b][X];
+    }
+    const T* yr = rowbase(tn, cn, b);
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int J = big_jorder<C, W>(q);
+      if (!((NEED >> J) & 1)) continue;
+#pragma unroll
+      for (int s = 0; s < TPW; ++s) {
+        int I = -1, J2 = -1;
+        big_tile<C>(W, s, I, J2);
+        if (I >= 0 && J2 == J) acc[s] = M::mma(wy[I], yb[b][J], acc[s]);
+      }
+      yb[b][J] = yr[16 * J];
+    }
+  };
+  // (the prologue issues its loads in the loop's order — columns, then rows — so the
+  // vmcnt waits the loop entry merges from both paths are the loop's own)
+#pragma unroll
+  for (int j = 0; j < CD; ++j) ldcol(j, cr[j]);
+  __builtin_amdgcn_sched_barrier(0);
+  gather(0, cr[0], 0);
+  __builtin_amdgcn_sched_barrier(0);
+  gather(1, cr[1], 1);
+  for (int t = 0; t < nsteps; t += CD) {
+#pragma unroll
+    for (int j = 0; j < CD; ++j) {
+      const int u = t + j;
+      __builtin_amdgcn_sched_barrier(0);
+      ldcol(u + CD, cr[j]);  // slot j held step u, gathered two steps ago
+      step(j & 1, u + 2, cr[(j + 2) % CD]);
+      // keep the loads beside the MFMAs that free their registers
+      [&]<int... Js>(std::integer_sequence<int, Js...>) {
+        auto grp = [&](auto Qc) {
+          constexpr int J = big_jorder<C, W>(decltype(Qc)::value);
+          if constexpr ((NEED >> J) & 1) {
+            constexpr int nm = [] {
+              int m = 0;
+              for (int s2 = 0; s2 < TPW; ++s2) {
+                int I = -1, J2 = -1;
+                big_tile<C>(W, s2, I, J2);
+                m += (I >= 0 && J2 == J);
+              }
+              return m;
+            }();
+            if constexpr (nm > 0) __builtin_amdgcn_sched_group_barrier(0x8, nm, 0);
+            __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+          }
+        };
+        (grp(std::integral_constant<int, Js>{}), ...);
+      }(std::make_integer_sequence<int, NT>{});
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Split Gram, MFMA side, for wave W (rows A = W, B = NT−1−W): each column block's planes
 // are read once per stage (three 16-B LDS reads per lane) and used for both rows.
 template <int NT, int W>
@@ -290,22 +452,29 @@ __device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m
 // solve (slot = heavy row of a.desc: the reduced image of the row's first segment in place of
 // G + λI and the Gram).  The reference loops a heavy row inside one thread
 // (WALSEngine.cpp:277-287); SURVEY.md §5 "long rows".
-template <typename T, int NT, int MODE = 0>
-__global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
+// WV ≥ 0: the body of wave WV alone, with its tile map at compile time (the streamed fp64
+// Gram: one wave-specialised copy of the whole row solve per wave, so no accumulator values
+// merge across the waves' code paths); WV = −1: one body for every wave (runtime tile map).
+template <typename T, int NT, int MODE, int WV>
+__device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T, NT>& S) {
   using C = BigCfg<T, NT>;
   using M = Mfma<T>;
   using acc_t = typename M::acc_t;
   using vec_t = T __attribute__((ext_vector_type(C::VEC)));
   constexpr int KP = C::KP, NW = C::NW, TPW = C::TPW, SIG = C::SIG;
   constexpr int CPR = C::CPR, TRIPS = C::TRIPS, PLD = C::PLD;
-  __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
 
   const int tid = threadIdx.x;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = WV >= 0 ? WV : __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const int64_t slot = a.row_begin + blockIdx.x;
+  // QMFX_TRACE phase stamps (thread 0, row solves only): start, G + λI loaded, Gram done,
+  // factorization done, backward solve done (direct-kernel record layout, tools/trace_analyze.py)
+  const bool trace = MODE == 0 && a.trace != nullptr && tid == 0;
+  uint64_t tr[5] = {0, 0, 0, 0, 0};
+  if (trace) tr[0] = __builtin_amdgcn_s_memtime();
   int64_t row, beg, end, seg0 = 0;
   if constexpr (MODE == 0) {
     row = a.order ? a.order[slot] : slot;
@@ -346,6 +515,10 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     }
   }
 
+  if (trace) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[1] = __builtin_amdgcn_s_memtime();
+  }
   // ---- Gram: A += Σ w y yᵀ, b = Σ c y, Σc -------------------------------------------------
   T bp = T(0);        // b[tid] for tid < KP
   double cs = 0.0;    // Σc (thread 0)
@@ -439,6 +612,35 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     if (tid == 0)
       for (int w = 0; w < 8; ++w) cs += S.cred[w];
     __syncthreads();
+  } else if constexpr (C::STREAM) {
+    const int n = (int)(end - beg);
+    auto gs = [&](auto wtag) {
+      constexpr int W = decltype(wtag)::value;
+      T bq[NT];
+#pragma unroll
+      for (int X = 0; X < NT; ++X) bq[X] = T(0);
+      big_gram_stream<T, NT, W>(a, beg, n, acc, bq, lane);
+      // the wave's blocks of b, summed over the four signal groups
+#pragma unroll
+      for (int X = 0; X < NT; ++X) {
+        if (big_b_owner<C>(X) == W) {
+          T v = bq[X];
+          v += shfl_xor(v, 16);
+          v += shfl_xor(v, 32);
+          if (kk == 0) S.bw[16 * X + cl] = v;
+        }
+      }
+      if constexpr (W == NW - 1) {  // Σc over the row's signals
+        double c = 0.0;
+        for (int e = lane; e < n; e += 64) c += (double)(T(1) + a.alpha * a.val[beg + e]);
+        c = wave_sum(c);
+        if (lane == 0) S.cred[0] = c;
+      }
+    };
+    dispatch_wave<NW>(wv, gs);
+    __syncthreads();
+    if (tid < KP) bp = S.bw[tid];
+    if (tid == 0) cs = S.cred[0];
   } else {
   int cols[TRIPS];
   vec_t stg[TRIPS];
@@ -562,6 +764,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   }
   __syncthreads();
 
+  if (trace) tr[2] = __builtin_amdgcn_s_memtime();
   // ---- Cholesky A = L Lᵀ with the forward solve of b folded in --------------------------
   int bad = negw ? 1 : 0;  // a negative weight: flagged for the pivoted re-solve
   for (int p = 0; p < NT; ++p) {
@@ -606,6 +809,7 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
   if (tid == 0) S.bad = bad;
   __syncthreads();
 
+  if (trace) tr[3] = __builtin_amdgcn_s_memtime();
   // ---- backward solve Lᵀ x = y ----------------------------------------------------------
   for (int I = NT - 1; I >= 0; --I) {
     T part = T(0);
@@ -659,6 +863,32 @@ __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveAr
     for (int w = 0; w < NW; ++w) t += S.red[w];
     a.rowloss[row] = bad ? 0.0 : cs - t;
     if (bad && a.status) a.status[row] = 1;
+  }
+  if constexpr (MODE == 0) {
+    if (trace) {
+      tr[4] = __builtin_amdgcn_s_memtime();
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* o = a.trace + 8 * slot;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) o[j] = tr[j];
+      o[5] = hw | ((uint64_t)xcc << 32);
+      o[6] = (uint64_t)(end - beg);
+      o[7] = (uint64_t)row;
+    }
+  }
+}
+
+template <typename T, int NT, int MODE = 0>
+__global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
+  using C = BigCfg<T, NT>;
+  __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
+  if constexpr (C::STREAM) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dispatch_wave<C::NW>(wv, [&](auto w) { big_row_body<T, NT, MODE, decltype(w)::value>(a, S); });
+  } else {
+    big_row_body<T, NT, MODE, -1>(a, S);
   }
 }
 
@@ -889,6 +1119,12 @@ hipError_t launch_heavy_reduce_big(double* part, double* partb, double* partc, c
     default: return hipErrorInvalidValue; \
   }
 
+#ifdef QMFX_BIG_DEV16
+// (register / ISA inspection builds only: the k = 256 instances alone)
+#undef QMFX_BIG_SWITCH
+#define QMFX_BIG_SWITCH(NTV, CALL) return NTV == 16 ? CALL(16) : hipErrorInvalidValue;
+#define QMFX_BIG_ROW_SWITCH(NTV, CALL) return NTV == 16 ? CALL(16) : hipErrorInvalidValue;
+#else
 // the row kernel takes k > 128 only (qmfx.cpp use_big_rows); the tiled YᵀY also fp64 k = 80..128
 #define QMFX_BIG_ROW_SWITCH(NTV, CALL)    \
   switch (NTV) {                          \
@@ -902,6 +1138,7 @@ hipError_t launch_heavy_reduce_big(double* part, double* partb, double* partc, c
     case 16: return CALL(16);             \
     default: return hipErrorInvalidValue; \
   }
+#endif
 hipError_t launch_wals_big(const SolveArgs<float>& a, int nt, hipStream_t s) {
 #define CALL(N) launch_big_nt<float, N>(a, s)
   QMFX_BIG_ROW_SWITCH(nt, CALL)
