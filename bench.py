@@ -47,9 +47,13 @@ CONFIGS = {
     "c3z": (10_000_000, 1_000_000, 550_000_000, 128, 3),
     # C5 with the same Zipf(1.0) item popularity: the split-K heavy rows at k = 256
     "c5z": (10_000_000, 1_000_000, 550_000_000, 256, 3),
+    # the ML-100K-shaped synthetic (Appendix C, seed 1234; the committed
+    # fixture tests/golden/ml100k_shape.npz), k = 30, 10 epochs = one step (bench_c1)
+    "c1": (943, 1682, 100_000, 30, 1234),
 }
 ZIPF = {"c3z": 1.0, "c5z": 1.0}
 BPR_CONFIGS = {"c4"}
+C1_EPOCHS, C1_THREADS = 10, 4  # wals.cpp defaults for C1: 10 epochs, the CPU path at nthreads=4
 LAM, ALPHA = 0.05, 40.0
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md
 PEAK_F64_TFLOPS = 78.6
@@ -393,45 +397,215 @@ def bench_bpr(args, rank, world):
                                "detail": {"host": host, "lr": lr_next,
                                           "eval_loss": closs / len(trip),
                                           "device_eval_loss_same_epoch": dloss}}
+    if rank == 0 and not args.no_parity:
+        # the update rule, exact: a sample of triplets (positives with their negatives) applied
+        # in sequence by qmfx_bpr_apply and by the oracle's BPREngine::update restatement
+        # (BPREngine.cpp:178-220) from the same factors (Hogwild epochs are statistical; SURVEY
+        # §0.7)
+        po, _ = oracle_lib()
+        rng = np.random.default_rng(seed + 9)
+        ns = 20000
+        sample = trip[rng.choice(len(trip), ns, replace=False)]
+        U0, I0 = ctx.factors(0), ctx.factors(1)
+        b0 = np.zeros(ni)
+        lr_s = lr * 0.9 ** (args.warmup + args.steps)
+        ctx.bpr_set_biases(b0)
+        ctx.bpr_apply(sample, lr_s, *lam, False)
+        U, I = U0.copy(), I0.copy()
+        po.bpr_update_seq(U, I, b0.copy(), sample, lr_s, *lam, False)
+        err = max(float(np.max(np.abs(ctx.factors(0) - U)) / np.max(np.abs(U))),
+                  float(np.max(np.abs(ctx.factors(1) - I)) / np.max(np.abs(I))))
+        tol = 1e-12 if args.precision == 64 else 1e-5
+        out["parity"] = {"check": "qmfx_bpr_apply vs the oracle's BPREngine::update, %d sampled "
+                                  "triplets in sequence from the device's factors" % ns,
+                         "max_rel_err": err, "tolerance": tol, "pass": bool(err <= tol)}
+        del U0, I0, U, I
     if rank == 0:
         print(json.dumps(out), flush=True)
 
 
-def roofline_classes(ctx, k, precision):
-    """Per kernel class: its LARGE launch (the side whose launches take longest: a class's
-    launches differ by side, e.g. the C3 direct kernel runs 187 ms in the item half and 69 us in
-    the user half), that launch's algorithmic flops and bytes over its
-    HIP-event time, the bound (MFMA when the launch's intensity is above the ridge, else HBM) and
-    the fraction of that peak."""
+def class_stats(ctx):
+    """The context's kernel-class accounting: {class name: {"total": stats, "side": {side:
+    stats}}} with stats = dict(ms, launches, flops, bytes) (qmfx_kernel_stats[_side])."""
+    out = {}
+    for cls, name in ((0, "direct"), (1, "whitened")):
+        out[name] = {"total": ctx.kernel_stats(cls),
+                     "side": {sd: ctx.kernel_stats_side(cls, sd) for sd in (0, 1)}}
+    return out
+
+
+def bench_c1(args, rank):
+    """C1 (BASELINE configs[0]): the reference's CPU-runnable case, `wals` on the ML-100K shape
+    (943 × 1682, 100K signals, Appendix C generator, seed 1234), k = 30, λ 0.05, α 40, the item
+    factors from the seeded distribution file, 10 epochs.  One step = the whole 10-epoch run
+    from the same initial factors (qmf/wals.cpp:52-107: set factors, optimize).  The ingest
+    (device grouping of the triples) is done once, before the timed steps.  cpu_baseline: the
+    reference-structure port, the same 10 epochs at nthreads = 4 (the config's definition);
+    parity: the device's per-epoch losses and final factors against the port's, and its
+    epoch-1 / epoch-10 losses against the reference's printed values."""
+    import qmf_amd
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ml100k_shape.npz"))
+    users, items = d["users"].astype(np.int64), d["items"].astype(np.int64)
+    values = d["values"].astype(np.float64)
+    init = d["init_e9"].astype(np.float64) / 1e9
+    nu0, ni0, nnz0, k, seed = CONFIGS["c1"]
+    ctx = qmf_amd.Context(k, args.precision, device=int(os.environ.get("LOCAL_RANK", "0")))
+    ctx.group_signals(users, items, values)
+    nu, ni = ctx.nusers, ctx.nitems
+    assert (nu, ni, len(users)) == (nu0, ni0, nnz0), (nu, ni, len(users))
+    I0 = init[: ni * k].reshape(ni, k)
+
+    def run():
+        ctx.set_factors(1, I0)
+        out = []
+        for _ in range(C1_EPOCHS):
+            ctx.wals_half(0, ALPHA, LAM)
+            out.append(ctx.wals_half(1, ALPHA, LAM) / nu / ni)
+        return out
+
+    for _ in range(args.warmup):
+        run()
+    ctx.reset_stats()
+    ctx.sync()
+    t1 = time.perf_counter()
+    losses = None
+    for _ in range(args.steps):
+        losses = run()
+    ctx.sync()
+    el = time.perf_counter() - t1
+    solves = (nu + ni) * C1_EPOCHS * args.steps
+    classes = roofline_classes(class_stats(ctx), k, args.precision,
+                               {sd: int(sum(ctx.row_classes(sd)["whitened"])) for sd in (0, 1)})
+    roof = roofline_object(classes)
+    roof["classes"] = classes
+    out = {
+        "metric": "WALS solves/sec and ms/epoch at k=%d; achieved fraction of HBM roofline" % k,
+        "value": round(solves / el, 1), "unit": "solves/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "ms_per_epoch": round(el / args.steps / C1_EPOCHS * 1e3, 3),
+        "higher_is_better": True, "scaling": "replicas", "vs_baseline": None,
+        "dtype": "f32" if args.precision == 32 else "f64",
+        "data": "synthetic ML-100K shape (SURVEY.md Appendix C generator, seed 1234; "
+                "tests/golden/ml100k_shape.npz), item factors from the seeded distribution file",
+        "config": {"workload": "c1: %d users x %d items, %d nnz, k=%d, lambda=%g, alpha=%g, "
+                               "%d epochs per step" % (nu, ni, len(users), k, LAM, ALPHA, C1_EPOCHS),
+                   "nusers": nu, "nitems": ni, "nnz": len(users), "nfactors": k,
+                   "epochs_per_step": C1_EPOCHS, "parallelism": "rows1"},
+        "roofline": roof, "loss": losses[-1], "env": engine_env(os.environ),
+    }
+    variant = qmf_amd._abi.build_variant()
+    if variant:
+        out["variant"] = variant
+    if rank == 0 and (args.cpu_baseline != "none" or not args.no_parity):
+        po, lapack = oracle_lib()
+        o = po.OracleWALS(users, items, values, k, LAM, ALPHA)
+        o.set_factors(1, I0)
+        t0 = time.perf_counter()
+        closs = o.optimize(C1_EPOCHS, C1_THREADS)
+        tcpu = time.perf_counter() - t0
+        if args.cpu_baseline != "none":
+            out["cpu_baseline"] = {
+                "value": round((nu + ni) * C1_EPOCHS / tcpu, 1), "unit": "solves/s",
+                "cores": C1_THREADS, "kind": "port", "ms_per_step": round(tcpu * 1e3, 1),
+                "sample": "the whole C1 run (10 epochs, nthreads=4, the config's definition) of the "
+                          "reference-structure port: %.2f s" % tcpu,
+                "detail": {"lapack": lapack, "host": cpu_share()[1]}}
+        if not args.no_parity:
+            err = max(float(np.max(np.abs(ctx.factors(sd) - o.factors(sd))) /
+                            np.max(np.abs(o.factors(sd)))) for sd in (0, 1))
+            lerr = max(abs(a - b) / abs(b) for a, b in zip(losses, closs))
+            ref = (float(d["ref_loss_epoch1"]), float(d["ref_loss_epoch10"]))
+            # after 10 epochs (tests/test_cli_gpu.py's bar): fp64 1e-8, fp32 north_star's 1e-4;
+            # the reference prints its losses to 6 significant digits
+            tol = 1e-8 if args.precision == 64 else 1e-4
+            out["parity"] = {
+                "max_factor_rel_err_vs_port": err, "max_epoch_loss_rel_err_vs_port": lerr,
+                "loss_epoch1": losses[0], "loss_epoch10": losses[-1],
+                "reference_printed_losses": ref, "tolerance": tol,
+                "pass": bool(err <= tol and abs(losses[0] - ref[0]) < 1e-5
+                             and abs(losses[-1] - ref[1]) < 1e-6)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def roofline_classes(stats, k, precision, whitened_rows=None):
+    """Per kernel class and side: the launch's algorithmic flops and bytes (the
+    class's rows' signals, gathered rows, X writes and rowptr; the YᵀY read runs in its own
+    kernel) over its HIP-event time, the bound (MFMA when the launch's intensity is above the
+    ridge, else HBM) and the fraction of that peak.  A class's top-level fields are its LARGE
+    launch's (the side whose launches take longest: the C3 direct kernel runs 187 ms in the item
+    half and 69 us in the user half); `per_side` has both.  whitened_rows[side]: the side's
+    n×n-route rows, whose x' round trip (written after the solve, read by the unwhitening pass:
+    2·k·s per row) is reported as `extra_bytes` beside the §8(d) bytes, not inside them."""
     peak_tf = PEAK_F32_TFLOPS if precision == 32 else PEAK_F64_TFLOPS
     ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
-    direct_name = "wals_big_kernel" if k > 128 else "wals_direct_kernel"
+    esz = 4 if precision == 32 else 8
+    names = {"direct": "wals_big_kernel" if k > 128 else "wals_direct_kernel",
+             "whitened": "wals_whitened (row solve + unwhiten)"}
     classes = {}
-    for cls, name in ((0, direct_name), (1, "wals_whitened (row solve + unwhiten)")):
-        tot = ctx.kernel_stats(cls)
+    for cls, name in names.items():
+        tot = stats[cls]["total"]
         if tot["launches"] == 0 or tot["ms"] <= 0:
             continue
         per = {}
         for side in (0, 1):
-            st = ctx.kernel_stats_side(cls, side)
-            if st["launches"] and st["ms"] > 0:
-                n = st["launches"]
-                per[side] = dict(launch_ms=st["ms"] / n, flops=st["flops"] / n, bytes=st["bytes"] / n)
+            st = stats[cls]["side"][side]
+            if not (st["launches"] and st["ms"] > 0):
+                continue
+            n = st["launches"]
+            ms, fl, by = st["ms"] / n, st["flops"] / n, st["bytes"] / n
+            sec = ms / 1e3
+            tf, gbs = fl / sec / 1e12, by / sec / 1e9
+            if fl / by >= ridge:
+                bound, ach, pk, unit = "mfma", tf, peak_tf, "TFLOP/s"
+            else:
+                bound, ach, pk, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
+            per[side] = dict(launch_ms=round(ms, 3), bound=bound, achieved=round(ach, 3), peak=pk,
+                             unit=unit, frac=round(ach / pk, 4), tflops=round(tf, 3),
+                             gbs=round(gbs, 1), flops_per_launch=fl, bytes_per_launch=by)
+            if cls == "whitened" and whitened_rows is not None:
+                per[side]["extra_bytes"] = float(2 * whitened_rows[side] * k * esz)
         side = max(per, key=lambda sd: per[sd]["launch_ms"])
-        p = per[side]
-        sec = p["launch_ms"] / 1e3
-        tf, gbs = p["flops"] / sec / 1e12, p["bytes"] / sec / 1e9
-        if p["flops"] / p["bytes"] >= ridge:
-            bound, ach, pk, unit = "mfma", tf, peak_tf, "TFLOP/s"
-        else:
-            bound, ach, pk, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
-        classes[name] = dict(side=side, launch_ms=round(p["launch_ms"], 3), bound=bound,
-                             achieved=round(ach, 3), peak=pk, unit=unit, frac=round(ach / pk, 4),
-                             tflops=round(tf, 3), gbs=round(gbs, 1), flops_per_launch=p["flops"],
-                             bytes_per_launch=p["bytes"], total_ms=round(tot["ms"], 3),
-                             launches=tot["launches"],
-                             per_side_launch_ms={sd: round(v["launch_ms"], 3) for sd, v in per.items()})
+        classes[name] = dict(per[side], side=side, total_ms=round(tot["ms"], 3),
+                             launches=tot["launches"], per_side=per,
+                             per_side_launch_ms={sd: v["launch_ms"] for sd, v in per.items()})
     return classes
+
+
+# the line's headline class: the one with the most kernel time, except that within this margin
+# the item half's class is named (C3 fp64's two classes tie within 0.1%: the headline flipped
+# between runs in round 5)
+HEADLINE_TIE = 0.05
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "launch_ms", "bytes_per_launch",
+             "flops_per_launch")
+
+
+def roofline_object(classes):
+    """The line's `roofline`: the headline class's fields, the weakest class, and both halves
+    as fixed fields (`user_half`, `item_half`: the class with the longer launch on that side,
+    with that side's launch figures)."""
+    order = sorted(classes, key=lambda n: classes[n]["total_ms"], reverse=True)
+    dom = order[0]
+    if len(order) > 1 and classes[order[1]]["total_ms"] >= (1 - HEADLINE_TIE) * classes[dom]["total_ms"]:
+        items = [n for n in order[:2] if classes[n]["side"] == 1]
+        if items:
+            dom = items[0]
+    weak = min(classes, key=lambda n: classes[n]["frac"])
+    d = classes[dom]
+    roof = {"kernel": dom, **{k: d[k] for k in ROOF_KEYS}, "launch_side": d["side"],
+            "weakest": {"kernel": weak, "bound": classes[weak]["bound"],
+                        "frac": classes[weak]["frac"], "launch_ms": classes[weak]["launch_ms"]}}
+    if "extra_bytes" in d:
+        roof["extra_bytes"] = d["extra_bytes"]
+    for side, field in ((0, "user_half"), (1, "item_half")):
+        on = [n for n in classes if side in classes[n]["per_side"]]
+        if on:
+            best = max(on, key=lambda n: classes[n]["per_side"][side]["launch_ms"])
+            ps = classes[best]["per_side"][side]
+            roof[field] = {"kernel": best, **{k: ps[k] for k in ROOF_KEYS}}
+            if "extra_bytes" in ps:
+                roof[field]["extra_bytes"] = ps["extra_bytes"]
+    return roof
 
 
 T_START = time.time()
@@ -558,6 +732,8 @@ def main():
     check_env(os.environ, variant, args.allow_variant)
     check_world(args.gpus, world, qmf_amd.device_count(), local)
     cpu_share()
+    if args.config == "c1":
+        return bench_c1(args, rank)
     if args.config in BPR_CONFIGS:
         # BPR shards nothing (Hogwild across GPUs would need cross-device atomics): every
         # rank runs an independent replica; rank 0 reports
@@ -609,17 +785,15 @@ def main():
     ms_epoch = el / args.steps * 1e3
     solves = (nu + ni) * args.steps
     value = solves / el
-    classes = roofline_classes(ctx, k, args.precision)
-    # the dominant class (most kernel time) carries the line's roofline; the class furthest
-    # below its own roofline is named beside it
-    dom = max(classes, key=lambda n: classes[n]["total_ms"])
-    weak = min(classes, key=lambda n: classes[n]["frac"])
+    wrows = {}
+    for sd in (0, 1):
+        wrows[sd] = int(sum(ctx.row_classes(sd)["whitened"]))  # this rank's n×n-route rows
+    classes = roofline_classes(class_stats(ctx), k, args.precision, wrows)
+    # the headline class (roofline_object) carries the line's roofline; the class furthest
+    # below its own roofline and both halves' classes are named beside it
+    roof = roofline_object(classes)
+    dom = roof["kernel"]
     d = classes[dom]
-    roof = {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
-            "unit": d["unit"], "frac": d["frac"], "launch_ms": d["launch_ms"],
-            "launch_side": d["side"],
-            "weakest": {"kernel": weak, "bound": classes[weak]["bound"],
-                        "frac": classes[weak]["frac"], "launch_ms": classes[weak]["launch_ms"]}}
     # PMC bytes of the same (large) launch, from the newest committed summary for this workload
     traffic, tsrc = pmc_traffic(args.config, args.precision, dom, k)
     roof.update({"traffic": round(traffic, 0) if traffic else None,

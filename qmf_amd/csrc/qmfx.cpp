@@ -1286,10 +1286,11 @@ int half_end(qmfx_ctx* c, double* loss_sum) {
     acc(0, ms_d, fl_d, by_d);
   }
   if (nW > 0 && use_w) {
-    // whitened-row flops precomputed per side in build_buckets; bytes: gathers, x' write,
-    // x' read + x write
+    // whitened-row flops precomputed per side in build_buckets; bytes as SURVEY.md §8(d):
+    // signals, gathered rows, X write, rowptr (the x' round trip of the unwhitening pass,
+    // 2·k·s per row, is reported beside them by bench.py as extra_bytes)
     fl_w = L.flops_w;
-    by_w = nzw * (4 + s) + nzw * k * s + nw * k * s * 3 + nw * 16;
+    by_w = nzw * (4 + s) + nzw * k * s + nw * k * s + (nw + 1) * 8;
     acc(1, ms_w, fl_w, by_w);
   }
   acc(2, ms_h, fl_d + fl_w, by_d + by_w);

@@ -26,6 +26,7 @@
 #pragma clang diagnostic ignored "-Wpass-failed"
 #include "kernels.h"
 #include "rowsolve.h"
+#include "chol.h"
 
 #ifndef QMFX_BIG_SIG32
 #define QMFX_BIG_SIG32 32
@@ -114,6 +115,7 @@ struct BigShared {
     struct {
       T panel[C::KP * C::PLD];
       T Ldiag[NT * 16 * C::PLD];
+      T panel2[C::STREAM ? C::KP * C::PLD : 1];  // LDLᵀ factorization: odd panels
     };
   };
   T w[2][C::SIG];   // α·v of the staged signals (0 past the row end)
@@ -446,6 +448,181 @@ __device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m
   l = uint2{pack_hi16(lo[0], lo[1]), pack_hi16(lo[2], lo[3])};
 }
 
+// LDLᵀ factorization and solves of the streamed (fp64) rows, for wave W (compile-time tile
+// map): chol.h's method (A = U D⁻¹ Uᵀ, U the unnormalised columns, one reciprocal per pivot,
+// the forward solve folded into the panel) spread over the workgroup.  Per 16-column panel p:
+//   (a) the owners of the panel's tiles store them to the panel buffer (two buffers in turn, so
+//       the next panel's stores need no barrier behind this panel's readers);
+//   (b) the waves with panel rows below the diagonal block (at most 4, one per SIMD; wave 0
+//       always) factor the panel column by column: the diagonal block sits in every 16-lane row
+//       of the wave, so column c's entries arrive by one v_fmac_f64_dpp row_newbcast per
+//       element (no readlane); lane q holds panel row 16 + 64W + q and its b entry.  Wave 0
+//       keeps 1/d, z and the transposed, scaled diagonal block for the backward solve;
+//   (c) the owners take U(I, p) back into their tiles and apply the rank-16 trailing update
+//       A(I, J) −= U(I, p) D⁻¹ U(J, p)ᵀ to their tiles with MFMA (operands from the buffer).
+// Then the backward solve by 16-blocks: the owners of tiles (J, I), J > I, add their part of
+// Uᵀx in LDS, and wave 0 finishes the block with one DPP FMA per column.
+// In: acc = lower tiles of A; S.bw = b.  Out: S.xs = x; `bad` (wave 0) on a pivot ∉ (0, ∞).
+template <typename T, int NT, int WI>
+__device__ __forceinline__ void big_ldl_solve(BigShared<T, NT>& S,
+                                              typename Mfma<T>::acc_t (&acc)[BigCfg<T, NT>::TPW],
+                                              int lane, int& bad, uint64_t* sub = nullptr) {
+  static_assert(sizeof(T) == 8, "the DPP panel form is fp64");
+  using C = BigCfg<T, NT>;
+  using M = Mfma<T>;
+  constexpr int KP = C::KP, TPW = C::TPW, PLD = C::PLD;
+  const int cl = lane & 15, kk = lane >> 4;
+  // (QMFX_BIG_SUBTRACE diagnostics builds: cycles of (a), (b), (c) and the backward solve)
+  uint64_t t0 = 0, ta = 0, tb = 0, tc = 0;
+  auto stamp = [&]() -> uint64_t { return sub ? __builtin_amdgcn_s_memtime() : 0; };
+  t0 = stamp();
+  for (int p = 0; p < NT; ++p) {
+    T* P = (p & 1) ? S.panel2 : S.panel;
+    const int R = KP - 16 * p;
+    // (a)
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      int I = -1, J = -1;
+      big_tile<C>(WI, s, I, J);
+      if (I >= 0 && J == p) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(16 * (I - p) + M::crow(lane, r)) * PLD + cl] = acc[s][r];
+      }
+    }
+    __syncthreads();
+    if (sub) {
+      const uint64_t t = stamp();
+      ta += t - t0;
+      t0 = t;
+    }
+    // (b)
+    if (WI == 0 || 16 + 64 * WI < R) {
+      const int q = 16 + 64 * WI + lane;
+      const bool live = q < R;
+      const int qq = live ? q : 0;
+      T dg[16], pa[16];
+      lds_row_load(&P[cl * PLD], dg);
+      T bdg = S.bw[16 * p + cl];
+      lds_row_load(&P[qq * PLD], pa);
+      T pb = S.bw[16 * p + qq];
+      T invv = T(0), zv = T(0);
+      [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+        (dg_column<Cs>(dg, bdg, pa, pb, true, cl, invv, zv), ...);
+      }(std::make_integer_sequence<int, 16>{});
+      if (live) {
+        lds_row_store(&P[q * PLD], pa);
+        S.bw[16 * p + q] = pb;
+      }
+      if (WI == 0) {
+        bad |= __any(lane < 16 && !(invv > T(0) && invv < __builtin_huge_val())) ? 1 : 0;
+        if (lane < 16) {
+          lds_row_store(&P[lane * PLD], dg);  // U of the diagonal block (for Lt below)
+          S.invd[16 * p + lane] = invv;
+          S.bw[16 * p + lane] = zv;
+        }
+      }
+    }
+    __syncthreads();
+    if (sub) {
+      const uint64_t t = stamp();
+      tb += t - t0;
+      t0 = t;
+    }
+    if (WI == C::NW - 1) {
+      // the diagonal block → Lt, transposed and scaled by 1/d of its row, negated:
+      // Lt[q][c] = −U[c][q]/d_q for c > q (the backward solve's DPP FMAs)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = lane + 64 * it;
+        const int r = idx >> 4, c = idx & 15;
+        S.Ldiag[(16 * p + c) * PLD + r] = c < r ? -(P[r * PLD + c] * S.invd[16 * p + c]) : T(0);
+      }
+    }
+    // (c)
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      int I = -1, J = -1;
+      big_tile<C>(WI, s, I, J);
+      if (I >= 0 && J == p && I > p) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[s][r] = P[(16 * (I - p) + M::crow(lane, r)) * PLD + cl];
+      }
+    }
+    T dcol[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) dcol[s4] = S.invd[16 * p + 4 * s4 + kk];
+#pragma unroll
+    for (int J = 1; J < NT; ++J) {
+      bool any = false;
+#pragma unroll
+      for (int s = 0; s < TPW; ++s) {
+        int I = -1, J2 = -1;
+        big_tile<C>(WI, s, I, J2);
+        any |= I >= 0 && J2 == J;
+      }
+      if (!any || J <= p) continue;
+      T sj[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) sj[s4] = P[(16 * (J - p) + cl) * PLD + 4 * s4 + kk] * dcol[s4];
+#pragma unroll
+      for (int s = 0; s < TPW; ++s) {
+        int I = -1, J2 = -1;
+        big_tile<C>(WI, s, I, J2);
+        if (I >= 0 && J2 == J) {
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc[s] = M::mma(-P[(16 * (I - p) + cl) * PLD + 4 * s4 + kk], sj[s4], acc[s]);
+        }
+      }
+    }
+    if (sub) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint64_t t = stamp();
+      tc += t - t0;
+      t0 = t;
+    }
+  }
+  // backward solve, Uᵀ x = D z by 16-blocks from the bottom
+  for (int I = NT - 1; I >= 0; --I) {
+    T part = T(0);
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      int I2 = -1, J = -1;
+      big_tile<C>(WI, s, I2, J);
+      if (I2 >= 0 && J == I && I2 > I) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part += acc[s][r] * S.xs[16 * I2 + M::crow(lane, r)];
+      }
+    }
+    part += shfl_xor(part, 16);
+    part += shfl_xor(part, 32);
+    if (kk == 0) S.part[WI * 16 + cl] = part;
+    __syncthreads();
+    if (WI == 0) {
+      T vm = S.bw[16 * I + cl];
+#pragma unroll
+      for (int w = 0; w < C::NW; ++w) vm -= S.part[w * 16 + cl];
+      vm *= S.invd[16 * I + cl];
+      T lt[16];
+      lds_row_load(&S.Ldiag[(16 * I + cl) * PLD], lt);
+      // x_c is lane c's vm in every 16-lane row: one DPP FMA per column (chol.h), two wait
+      // states first (vm was just written by a VALU the hazard recognizer sees, read by asm)
+      asm volatile("s_nop 1" : "+v"(vm));
+      [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+        (fmac_bcast16<15 - Cs, 1>(vm, vm, lt[15 - Cs]), ...);
+      }(std::make_integer_sequence<int, 16>{});
+      if (lane < 16) S.xs[16 * I + lane] = vm;
+    }
+    __syncthreads();
+  }
+  if (sub) {
+    sub[0] = ta;
+    sub[1] = tb;
+    sub[2] = tc;
+    sub[3] = stamp() - t0;
+  }
+}
+
 // MODE (compile time, as in the one-wave direct kernel): 0 = row solve; 1 = split-K segment
 // Gram (slot = segment of a.desc: the Gram of its signals from zero, written as tile images
 // + rhs + Σc + flag to the segment's part/partb/partc slot, no solve); 2 = split-K heavy-row
@@ -767,6 +944,19 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
   if (trace) tr[2] = __builtin_amdgcn_s_memtime();
   // ---- Cholesky A = L Lᵀ with the forward solve of b folded in --------------------------
   int bad = negw ? 1 : 0;  // a negative weight: flagged for the pivoted re-solve
+#ifdef QMFX_BIG_SUBTRACE
+  uint64_t sub[4] = {0, 0, 0, 0};
+#endif
+  if constexpr (C::STREAM && WV >= 0) {
+#ifdef QMFX_BIG_SUBTRACE
+    big_ldl_solve<T, NT, WV>(S, acc, lane, bad, trace ? sub : nullptr);
+#else
+    big_ldl_solve<T, NT, WV>(S, acc, lane, bad);
+#endif
+    if (tid == 0) S.bad = bad;
+    __syncthreads();
+    if (trace) tr[3] = __builtin_amdgcn_s_memtime();
+  } else {
   for (int p = 0; p < NT; ++p) {
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {
@@ -846,6 +1036,7 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
     }
     __syncthreads();
   }
+  }  // LDLᵀ / Cholesky
 
   // ---- output: x, row loss = Σc − xᵀb − λ‖x‖² ----------------------------------------------
   double xb = 0.0, xx = 0.0;
@@ -874,6 +1065,16 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
 #pragma unroll
       for (int j = 0; j < 5; ++j) o[j] = tr[j];
       o[5] = hw | ((uint64_t)xcc << 32);
+#ifdef QMFX_BIG_SUBTRACE
+      if constexpr (C::STREAM && WV >= 0) {
+        // diagnostics record: start, (a), (b), (c), backward, Gram cycles, n, row
+        o[1] = sub[0];
+        o[2] = sub[1];
+        o[3] = sub[2];
+        o[4] = sub[3];
+        o[5] = tr[2] - tr[1];
+      }
+#endif
       o[6] = (uint64_t)(end - beg);
       o[7] = (uint64_t)row;
     }

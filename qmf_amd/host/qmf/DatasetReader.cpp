@@ -1,5 +1,7 @@
 #include <qmf/DatasetReader.h>
 
+#include <cctype>
+#include <charconv>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -21,7 +23,7 @@ namespace {
 // "%lld %lld %lf" on [b, e) (e points at the line terminator, not included).  Returns
 // false when fewer than three conversions succeed, like sscanf's result != 3.  The buffer
 // is copied into a small NUL-terminated scratch so strtoll/strtod cannot run past the line.
-bool parseLine(const char* b, const char* e, DatasetElem& elem, std::string& scratch) {
+bool parseLineCopy(const char* b, const char* e, DatasetElem& elem, std::string& scratch) {
   scratch.assign(b, e);
   const char* p = scratch.c_str();
   char* q = nullptr;
@@ -36,6 +38,37 @@ bool parseLine(const char* b, const char* e, DatasetElem& elem, std::string& scr
   if (q == p) return false;
   elem.userId = u;
   elem.itemId = i;
+  elem.value = static_cast<Double>(v);
+  return true;
+}
+
+inline bool isSpace(char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+
+// The same conversion in place, without the copy: std::from_chars reads [b, e) directly and
+// rounds like strtod / strtoll on plain decimal fields.  Anything it does not take the way
+// sscanf would (a '+' sign, hex or inf/nan values, overflow, a field it rejects) goes to
+// parseLineCopy, so the result is sscanf's in every case.
+bool parseLine(const char* b, const char* e, DatasetElem& elem, std::string& scratch) {
+  const char* p = b;
+  long long f[2];
+  for (int j = 0; j < 2; ++j) {
+    while (p < e && isSpace(*p)) ++p;
+    const auto r = std::from_chars(p, e, f[j]);
+    if (r.ec != std::errc() || (r.ptr < e && !isSpace(*r.ptr)))
+      return parseLineCopy(b, e, elem, scratch);
+    p = r.ptr;
+  }
+  while (p < e && isSpace(*p)) ++p;
+  double v = 0.0;
+  const auto r = std::from_chars(p, e, v, std::chars_format::general);
+  // a value field must end the number the way strtod would (whitespace, end of line, or a
+  // character strtod also stops at); hex / inf / nan / '+' forms and range errors take the
+  // exact path
+  if (r.ec != std::errc() || r.ptr == p || (r.ptr < e && (isalnum((unsigned char)*r.ptr) ||
+                                                          *r.ptr == '.' || *r.ptr == 'x')))
+    return parseLineCopy(b, e, elem, scratch);
+  elem.userId = f[0];
+  elem.itemId = f[1];
   elem.value = static_cast<Double>(v);
   return true;
 }

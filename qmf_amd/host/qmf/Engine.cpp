@@ -1,5 +1,7 @@
 #include <qmf/Engine.h>
 
+#include <charconv>
+
 #include <algorithm>
 #include <cstdio>
 #include <fstream>
@@ -122,30 +124,35 @@ void Engine::computeTestRanks(qmfx_ctx* ctx, bool useBiases,
 
 namespace {
 
+// " %.9f" of x appended to s.  std::to_chars with a precision renders the exact decimal value
+// of x correctly rounded, as glibc's printf does, so the text is the same byte for byte (the
+// host tests compare them over random and edge values); a value that does not fit the buffer
+// (|x| ≥ 1e290) takes printf itself.
+inline void appendFixed9(std::string& s, Double x) {
+  char buf[320];
+  buf[0] = ' ';
+  const auto r = std::to_chars(buf + 1, buf + sizeof(buf), x, std::chars_format::fixed, 9);
+  if (r.ec == std::errc()) {
+    s.append(buf, r.ptr);
+    return;
+  }
+  std::string big(static_cast<size_t>(std::snprintf(nullptr, 0, " %.9f", x)) + 1, '\0');
+  std::snprintf(&big[0], big.size(), " %.9f", x);
+  big.pop_back();
+  s += big;
+}
+
 // Formats rows [b, e) exactly as `out << std::fixed << std::setprecision(9)` would:
 // libstdc++ renders fixed doubles through printf("%.*f").
 void formatRows(const FactorData& fd, const IdIndex& index, size_t b, size_t e, std::string& s) {
-  char buf[64];
+  char buf[32];
   const size_t k = fd.nfactors();
+  s.reserve(s.size() + (e - b) * (k * 13 + 24));
   for (size_t idx = b; idx < e; ++idx) {
-    int n = std::snprintf(buf, sizeof(buf), "%lld", static_cast<long long>(index.id(idx)));
-    s.append(buf, n);
-    if (fd.withBiases()) {
-      n = std::snprintf(buf, sizeof(buf), " %.9f", fd.biasAt(idx));
-      s.append(buf, n);
-    }
+    s.append(buf, std::to_chars(buf, buf + sizeof(buf), static_cast<long long>(index.id(idx))).ptr);
+    if (fd.withBiases()) appendFixed9(s, fd.biasAt(idx));
     const Double* row = fd.getFactors().data(idx);
-    for (size_t f = 0; f < k; ++f) {
-      n = std::snprintf(buf, sizeof(buf), " %.9f", row[f]);
-      if (n < 0 || n >= static_cast<int>(sizeof(buf))) {  // |x| ≥ 1e52: rare, exact path
-        std::string big(static_cast<size_t>(std::snprintf(nullptr, 0, " %.9f", row[f])) + 1, '\0');
-        std::snprintf(&big[0], big.size(), " %.9f", row[f]);
-        big.pop_back();
-        s += big;
-      } else {
-        s.append(buf, n);
-      }
-    }
+    for (size_t f = 0; f < k; ++f) appendFixed9(s, row[f]);
     s.push_back('\n');
   }
 }

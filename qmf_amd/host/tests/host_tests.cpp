@@ -215,13 +215,25 @@ TEST(DatasetReader, parallelFileParseEqualsSequential) {
     const long long u = (long long)(g() % 2000000) - 1000000;
     const long long i = (long long)(g() >> 1);
     char vb[64];
-    const int kind = (int)(g() % 4);
+    // (kinds 4-9: the forms the in-place parser hands to the strtod path — hex, inf / nan,
+    // out of range, subnormal, trailing garbage — and a fraction strtoll stops at)
+    const int kind = (int)(g() % 10);
     if (kind == 0) std::snprintf(vb, sizeof vb, "%d", (int)(g() % 6));
     if (kind == 1) std::snprintf(vb, sizeof vb, "%.17g", (double)(g() % 100000) / 7.0);
     if (kind == 2) std::snprintf(vb, sizeof vb, "%.3e", -(double)(g() % 1000));
     if (kind == 3) std::snprintf(vb, sizeof vb, "+%u.5", (unsigned)(g() % 9));
+    if (kind == 4) std::snprintf(vb, sizeof vb, "0x1.8p%d", (int)(g() % 8));
+    if (kind == 5) std::snprintf(vb, sizeof vb, "%s", (g() & 1) ? "inf" : "-nan");
+    if (kind == 6) std::snprintf(vb, sizeof vb, "1e%d", 300 + (int)(g() % 20));
+    if (kind == 7) std::snprintf(vb, sizeof vb, "%.3e", 1e-300 * (double)(g() % 1000) * 1e-10);
+    if (kind == 8) std::snprintf(vb, sizeof vb, "%u.25abc,x", (unsigned)(g() % 9));
+    if (kind == 9) std::snprintf(vb, sizeof vb, ".%u", (unsigned)(g() % 100));
+    // (the item field occasionally carries a fraction: "%lld" stops at the '.', and "%lf"
+    // then reads the fraction as the value — the value field is dropped by the scan)
+    const bool frac = g() % 16 == 0;
     text += (g() % 3 == 0 ? " " : "") + std::to_string(u) + sep[g() % 4] + std::to_string(i) +
-            sep[g() % 4] + vb + (g() % 5 == 0 ? "\r\n" : "\n");
+            (frac ? std::string(".75") : std::string("")) + sep[g() % 4] + vb +
+            (g() % 5 == 0 ? "\r\n" : "\n");
   }
   text += "42 43 44";  // last line without newline
   const std::string p = tmpPath("ds");
@@ -453,7 +465,15 @@ TEST(Engine, saveFactors) {
   for (size_t i = 0; i < n; ++i) big.getOrSetIdx((int64_t)(g() >> 2) - (int64_t)(i % 3) * (1LL << 60));
   FactorData fd(n, 3, true);
   std::normal_distribution<Double> nd(0.0, 1.0);
-  fd.setFactors([&](size_t i, size_t) { return i % 977 == 0 ? -0.0 : nd(g) * std::pow(10.0, (double)(i % 13) - 4); });
+  // (the writer formats with std::to_chars: every magnitude from 1e-14 to 1e22, values on a
+  // %.9f rounding boundary, ±0, ±inf, NaN and 1e300 — printf's own path — must match)
+  const Double special[] = {-0.0, 0.0, 0.0000000005, -0.0000000015, 2.5e-10, 0.1234567895,
+                            1e15 + 0.5, 1e22, -1e300, INFINITY, -INFINITY, NAN, 4.9e-324};
+  fd.setFactors([&](size_t i, size_t j) {
+    if (i % 977 == 0) return -0.0;
+    if (i % 101 == 0) return special[(i / 101 + j) % (sizeof(special) / sizeof(special[0]))];
+    return nd(g) * std::pow(10.0, (double)(i % 37) - 14);
+  });
   fd.setBiases([&](size_t) { return nd(g); });
   std::ostringstream fast, ref;
   EngineTestPeer::saveFactors(fd, big, fast);

@@ -1,5 +1,8 @@
 // `wals` command line, drop-in for the reference's qmf/wals.cpp:26-107: same flags, same
 // log lines and output files.  Additions: --device, --precision (32 | 64), --ngpus.
+#include <chrono>
+#include <cstdlib>
+#include <fstream>
 #include <memory>
 
 #include <qmf/DatasetReader.h>
@@ -38,6 +41,22 @@ DEFINE_bool(test_always, false,
 DEFINE_string(user_factors, "", "filename of user factors");
 DEFINE_string(item_factors, "", "filename of item factors");
 
+namespace {
+// QMF_TIMINGS=1 (an addition; unset, the output is the reference's): one "timing:" log line per
+// phase with its wall time, read by tools/bench_cli.py
+bool timings() {
+  static const bool on = std::getenv("QMF_TIMINGS") && std::atoi(std::getenv("QMF_TIMINGS")) > 0;
+  return on;
+}
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+long long fileBytes(const std::string& f) {
+  std::ifstream s(f, std::ios::binary | std::ios::ate);
+  return s ? static_cast<long long>(s.tellg()) : 0;
+}
+}  // namespace
+
 int main(int argc, char** argv) {
   if (!qmf::flags::parse(&argc, &argv, "wals")) return 1;
   if (FLAGS_user_factors.empty() || FLAGS_item_factors.empty()) {
@@ -61,19 +80,34 @@ int main(int argc, char** argv) {
   qmf::WALSEngine engine(config, metricsEngine, static_cast<size_t>(FLAGS_nthreads), device);
 
   LOG(INFO) << "loading training data";
+  double t0 = now();
   qmf::DatasetReader trainReader(FLAGS_train_dataset);
-  engine.init(trainReader.readAll());
+  {
+    const auto data = trainReader.readAll();
+    const double t1 = now();
+    if (timings())
+      LOG(INFO) << "timing: parse " << t1 - t0 << " s, " << fileBytes(FLAGS_train_dataset)
+                << " bytes, " << data.size() << " lines";
+    engine.init(data);
+    if (timings()) LOG(INFO) << "timing: init " << now() - t1 << " s";
+  }
   if (!FLAGS_test_dataset.empty()) {
     LOG(INFO) << "loading test data";
     qmf::DatasetReader testReader(FLAGS_test_dataset);
     engine.initTest(testReader.readAll());
   }
   LOG(INFO) << "training";
+  t0 = now();
   engine.optimize();
+  if (timings()) LOG(INFO) << "timing: optimize " << now() - t0 << " s, " << FLAGS_nepochs << " epochs";
   if (!FLAGS_user_factors.empty() && !FLAGS_item_factors.empty()) {
     LOG(INFO) << "saving model output";
+    t0 = now();
     engine.saveUserFactors(FLAGS_user_factors);
     engine.saveItemFactors(FLAGS_item_factors);
+    if (timings())
+      LOG(INFO) << "timing: save " << now() - t0 << " s, "
+                << fileBytes(FLAGS_user_factors) + fileBytes(FLAGS_item_factors) << " bytes";
   }
   return 0;
 }

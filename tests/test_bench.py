@@ -121,3 +121,42 @@ def test_exchange_fields_are_max_over_ranks_gloo_world2():
     assert set(f) == {"user_half", "item_half"}
     assert f["user_half"] == {"exchange_ms": 11.0, "exposed_ms": 2.0, "solve_ms": 20.0}
     assert f["item_half"] == {"exchange_ms": 12.0, "exposed_ms": 2.0, "solve_ms": 20.0}
+
+
+def _fake_stats(d_ms, w_ms, d_side_ms, w_side_ms):
+    """class_stats()-shaped accounting: per class the total and per-side figures (two launches
+    per side; the *_side_ms arguments are per launch)."""
+    def st(ms, launches, fl, by):
+        return dict(ms=ms, launches=launches, flops=fl, bytes=by)
+    return {
+        "direct": {"total": st(d_ms, 4, 0, 0),
+                   "side": {0: st(2 * d_side_ms[0], 2, 2 * 1e9, 2 * 1e9),
+                            1: st(2 * d_side_ms[1], 2, 2 * 9.12e12, 2 * 5.3e11)}},
+        "whitened": {"total": st(w_ms, 2, 0, 0),
+                     "side": {0: st(2 * w_side_ms[0], 2, 2 * 5e11, 2 * 528.3e9),
+                              1: st(0, 0, 0, 0)}},
+    }
+
+
+def test_roofline_fields_are_fixed_per_half():
+    """both halves are first-class fields; the headline does not flip on a tie
+    (C3 fp64: whitened 3531.5 vs direct 3530.4 ms)."""
+    st = _fake_stats(3530.4, 3531.5, (0.07, 176.4), (176.6, 0))
+    classes = bench.roofline_classes(st, 128, 64, whitened_rows={0: 9_900_000, 1: 0})
+    roof = bench.roofline_object(classes)
+    assert roof["kernel"] == "wals_direct_kernel" and roof["launch_side"] == 1  # tie → item half
+    assert set(roof) >= {"kernel", "bound", "achieved", "peak", "unit", "frac", "launch_ms",
+                         "bytes_per_launch", "flops_per_launch", "launch_side", "weakest",
+                         "user_half", "item_half"}
+    uh, ih = roof["user_half"], roof["item_half"]
+    assert uh["kernel"] == "wals_whitened (row solve + unwhiten)" and uh["bound"] == "hbm"
+    assert ih["kernel"] == "wals_direct_kernel" and ih["bound"] == "mfma"
+    # §8(d) bytes over the launch time, the x' round trip beside them (not inside)
+    assert abs(uh["achieved"] - 528.3e9 / 0.1766 / 1e9) < 1.0
+    assert uh["extra_bytes"] == 2 * 9_900_000 * 128 * 8
+    assert abs(ih["frac"] - 9.12e12 / 0.1764 / 1e12 / bench.PEAK_F64_TFLOPS) < 1e-3
+    # a clear winner is named whatever its side
+    st2 = _fake_stats(1000.0, 3000.0, (0.07, 500.0), (1500.0, 0))
+    roof2 = bench.roofline_object(bench.roofline_classes(st2, 128, 64))
+    assert roof2["kernel"] == "wals_whitened (row solve + unwhiten)"
+    assert roof2["user_half"]["kernel"] == roof2["kernel"]
