@@ -43,6 +43,9 @@
 #ifndef QMFX_BIG_STREAM
 #define QMFX_BIG_STREAM 1  // fp64: per-wave streamed Gram (0: the LDS-staged Gram)
 #endif
+#ifndef QMFX_BIG_LDL32
+#define QMFX_BIG_LDL32 1  // fp32 k = 256: wave-specialised rows with the LDLᵀ (0: the Cholesky)
+#endif
 #ifndef QMFX_BIG_PAIR64
 #define QMFX_BIG_PAIR64 1  // fp64 k = 256: row-pair tile map (0: round-robin)
 #endif
@@ -66,6 +69,9 @@ struct BigCfg {
   static constexpr bool STREAM = sizeof(T) == 8 && QMFX_BIG_STREAM;
   // row-pair tile map (wave W owns block rows W and NT−1−W: NT + 1 tiles)
   static constexpr bool PAIR = SPLIT || (STREAM && NT == 2 * NW && QMFX_BIG_PAIR64);
+  // one wave-specialised copy of the row solve per wave (compile-time tile map) and the LDLᵀ
+  // factorization (big_ldl_solve): the streamed fp64 rows and the split fp32 rows
+  static constexpr bool WSPEC = STREAM || (SPLIT && QMFX_BIG_LDL32);
   static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
@@ -73,7 +79,8 @@ struct BigCfg {
   static constexpr int VEC = 16 / sizeof(T);             // elements per 16-B load
   static constexpr int CPR = KP / VEC;                   // 16-B chunks per row
   static constexpr int TRIPS = (SIG * CPR + NTHR - 1) / NTHR;
-  static constexpr int PLD = 17;                         // padded LDS row of a panel
+  // padded LDS row of a panel (fp32: 16-B aligned rows for the b128 row accesses)
+  static constexpr int PLD = sizeof(T) == 4 ? 20 : 17;
   // compile-time tile map with LDS fragments reused across a wave's tiles (Gram and
   // trailing update); the fp64 tilings above NT = 11 lack the registers for it
   static constexpr bool REUSE = sizeof(T) == 4 || NT <= 11;
@@ -115,7 +122,7 @@ struct BigShared {
     struct {
       T panel[C::KP * C::PLD];
       T Ldiag[NT * 16 * C::PLD];
-      T panel2[C::STREAM ? C::KP * C::PLD : 1];  // LDLᵀ factorization: odd panels
+      T panel2[C::WSPEC ? C::KP * C::PLD : 1];  // LDLᵀ factorization: odd panels
     };
   };
   T w[2][C::SIG];   // α·v of the staged signals (0 past the row end)
@@ -448,6 +455,41 @@ __device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m
   l = uint2{pack_hi16(lo[0], lo[1]), pack_hi16(lo[2], lo[3])};
 }
 
+// fp32 twin of chol.h's bcast16 (lane J of every 16-lane row)
+template <int J>
+__device__ __forceinline__ float bcast16(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xf, 0xf, false));
+}
+// Column C of a panel in the replicated-diagonal layout (chol.h dg_column, for either precision):
+// the pivot d = U[C][C] and z_C = b_C broadcast from lane C of every 16-lane row, the
+// right-hand sides' update, and the trailing columns m > C of the diagonal block and of the
+// lane's panel row, each element one v_fmac_dpp row_newbcast of column C's entry U[m][C].
+template <int C, typename T>
+__device__ __forceinline__ void big_dg_column(T (&dg)[16], T& bdg, T (&pa)[16], T& pb, int cl,
+                                              T& invv, T& zv) {
+  const T d = bcast16<C>(dg[C]);
+  const T bc = bcast16<C>(bdg);
+  const T invd = pivot_rcp(d);
+  const bool me = cl == C;
+  invv = me ? invd : invv;
+  zv = me ? bc : zv;
+  const T nl = -(dg[C] * invd);
+  const T nls = -(pa[C] * invd);
+  bdg = __builtin_fma(nl, bc, bdg);
+  pb = __builtin_fma(nls, bc, pb);
+  [&]<int... Ms>(std::integer_sequence<int, Ms...>) {
+    auto upd = [&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      if constexpr (m > C) {
+        fmac_bcast16<m, (m == C + 1) ? 1 : 0>(dg[m], dg[C], nl);
+        fmac_bcast16<m>(pa[m], dg[C], nls);
+      }
+    };
+    (upd(std::integral_constant<int, Ms>{}), ...);
+  }(std::make_integer_sequence<int, 16>{});
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // LDLᵀ factorization and solves of the streamed (fp64) rows, for wave W (compile-time tile
 // map): chol.h's method (A = U D⁻¹ Uᵀ, U the unnormalised columns, one reciprocal per pivot,
 // the forward solve folded into the panel) spread over the workgroup.  Per 16-column panel p:
@@ -467,7 +509,6 @@ template <typename T, int NT, int WI>
 __device__ __forceinline__ void big_ldl_solve(BigShared<T, NT>& S,
                                               typename Mfma<T>::acc_t (&acc)[BigCfg<T, NT>::TPW],
                                               int lane, int& bad, uint64_t* sub = nullptr) {
-  static_assert(sizeof(T) == 8, "the DPP panel form is fp64");
   using C = BigCfg<T, NT>;
   using M = Mfma<T>;
   constexpr int KP = C::KP, TPW = C::TPW, PLD = C::PLD;
@@ -507,7 +548,7 @@ __device__ __forceinline__ void big_ldl_solve(BigShared<T, NT>& S,
       T pb = S.bw[16 * p + qq];
       T invv = T(0), zv = T(0);
       [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
-        (dg_column<Cs>(dg, bdg, pa, pb, true, cl, invv, zv), ...);
+        (big_dg_column<Cs>(dg, bdg, pa, pb, cl, invv, zv), ...);
       }(std::make_integer_sequence<int, 16>{});
       if (live) {
         lds_row_store(&P[q * PLD], pa);
@@ -947,7 +988,7 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
 #ifdef QMFX_BIG_SUBTRACE
   uint64_t sub[4] = {0, 0, 0, 0};
 #endif
-  if constexpr (C::STREAM && WV >= 0) {
+  if constexpr (C::WSPEC && WV >= 0) {
 #ifdef QMFX_BIG_SUBTRACE
     big_ldl_solve<T, NT, WV>(S, acc, lane, bad, trace ? sub : nullptr);
 #else
@@ -1066,7 +1107,7 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
       for (int j = 0; j < 5; ++j) o[j] = tr[j];
       o[5] = hw | ((uint64_t)xcc << 32);
 #ifdef QMFX_BIG_SUBTRACE
-      if constexpr (C::STREAM && WV >= 0) {
+      if constexpr (C::WSPEC && WV >= 0) {
         // diagnostics record: start, (a), (b), (c), backward, Gram cycles, n, row
         o[1] = sub[0];
         o[2] = sub[1];
@@ -1085,7 +1126,7 @@ template <typename T, int NT, int MODE = 0>
 __global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
   using C = BigCfg<T, NT>;
   __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
-  if constexpr (C::STREAM) {
+  if constexpr (C::WSPEC) {
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     dispatch_wave<C::NW>(wv, [&](auto w) { big_row_body<T, NT, MODE, decltype(w)::value>(a, S); });
   } else {
