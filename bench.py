@@ -680,17 +680,36 @@ def check_env(environ, variant, allow_variant=False):
                          "pass --allow-variant to measure it anyway (the line is marked)" % variant)
 
 
-def exchange_fields(stats, steps, reduce_max):
+# the exchange model of DESIGN.md §6: a rank receives (W − 1)/W of the solved side's factor
+# matrix per half; "bus" is the all-gather bus rate RCCL reaches on 8-GPU MI300-class nodes
+# (an assumption the first SCALE run tests), "links" the receive bound of a fully connected
+# 8-GPU xGMI mesh (7 links × 153 GB/s)
+MODEL_BUS_GBS, MODEL_LINKS_GBS = 350.0, 1071.0
+
+
+def exchange_model(nrows, kp, esz, world):
+    """Predicted per-half exchange: bytes received per rank and their time at the model rates."""
+    b = nrows * kp * esz * (world - 1) / world
+    return {"bytes_in_per_rank": float(b), "model_ms_bus": round(b / MODEL_BUS_GBS / 1e6, 3),
+            "model_ms_links": round(b / MODEL_LINKS_GBS / 1e6, 3)}
+
+
+def exchange_fields(stats, steps, reduce_max, model=None):
     """Per half (users, items) of a multi-rank run: the exchange on the collective stream and
     the row solves, ms per half, each the max over ranks (reduce_max: list of floats -> the
     elementwise max over ranks).  stats[side] = Context.exchange_stats(side) (sums over the
-    timed halves)."""
+    timed halves); model[side] = exchange_model(...) of that half, printed beside the measured
+    exchange so the first multi-GPU record tests DESIGN.md §6 directly."""
     keys = ("exchange_ms", "exposed_ms", "solve_ms")
     vals = [stats[side][k] / max(steps, 1) for side in (0, 1) for k in keys]
     vals = reduce_max(vals)
     out = {}
     for side, name in ((0, "user_half"), (1, "item_half")):
         out[name] = {k: round(vals[3 * side + i], 3) for i, k in enumerate(keys)}
+        if model is not None:
+            out[name]["predicted"] = model[side]
+            bus = model[side]["bytes_in_per_rank"] / max(out[name]["exchange_ms"], 1e-9) / 1e6
+            out[name]["measured_gbs_in_per_rank"] = round(bus, 1)
     return out
 
 
@@ -810,8 +829,11 @@ def main():
             t = torch.tensor(vals, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return [float(v) for v in t]
+        kp = (k + 15) // 16 * 16
+        esz = 4 if args.precision == 32 else 8
+        model = {0: exchange_model(nu, kp, esz, world), 1: exchange_model(ni, kp, esz, world)}
         xfields = exchange_fields({sd: ctx.exchange_stats(sd) for sd in (0, 1)}, args.steps,
-                                  reduce_max)
+                                  reduce_max, model)
     half = ctx.kernel_stats(2)
     epoch_bytes = half["bytes"] / max(half["launches"], 1) * 2
     hbm_frac_epoch = epoch_bytes / (ms_epoch / 1e3) / (PEAK_HBM_GBS * 1e9)

@@ -79,7 +79,8 @@ int qmfx_gen_synthetic_zipf(qmfx_ctx* ctx, int64_t nusers, int64_t nitems, int64
 /* dst takes src's interactions (shape, id tables and both CSR orientations, copied device to
  * device: over xGMI between GPUs) instead of building them again: one qmfx_group_signals for
  * an n-GPU engine, then an import per peer before qmfx_dist_init_all shards them.  Both
- * contexts must have the same precision; src must not be sharded. */
+ * contexts must have the same precision; src must not be sharded and dst must not have been
+ * through qmfx_dist_init[_all].  src's stream is synchronised before the copies. */
 int qmfx_import_signals(qmfx_ctx* dst, qmfx_ctx* src);
 /* Copies a side's CSR back to the host (e.g. for CPU baselines on the same data).  values are
  * returned in double, exactly as the device holds them (an fp32 context's values widened). */

@@ -75,10 +75,12 @@ __device__ __forceinline__ void lds_row_store(T* dst, const T (&v)[16]) {
 #ifndef QMFX_BW_DPP
 #define QMFX_BW_DPP 1
 #endif
-// LDS ordering inside chol_solve.  Every caller's workgroup is one wave, and LDS accesses of
-// one wave execute in order, so draining them and pinning the compiler's order is enough (no
-// s_barrier; the same speed as a plain compiler fence in the micro-benchmark,
-// tools/exp/chol_bench.hip).  WS is kept for callers that document a multi-wave workgroup.
+// LDS ordering inside chol_solve.  chol_solve REQUIRES a single-wave workgroup: LDS accesses
+// of one wave execute in order, so draining them and pinning the compiler's order is enough
+// (no s_barrier; the same speed as a plain compiler fence in the micro-benchmark,
+// tools/exp/chol_bench.hip).  Both WS values behave the same — there is no workgroup barrier
+// here — and a multi-wave caller would race on S.panel and S.bw (debug builds trap on one,
+// chol_solve below).
 template <bool WS>
 __device__ __forceinline__ void csync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -218,6 +220,9 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
   const int cl = lane & 15;
   const int kk = lane >> 4;
   const int q0 = DG ? 16 : 0;  // first panel row held by slot 0
+#ifdef QMFX_DEBUG
+  if (blockDim.x * blockDim.y * blockDim.z != 64) __builtin_trap();  // single-wave callers only
+#endif
 #pragma unroll
   for (int p = 0; p < NT; ++p) {
     const int R = KP - 16 * p;

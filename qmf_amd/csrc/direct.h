@@ -198,6 +198,12 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_F64_ASM
 #define QMFX_F64_ASM 1
 #endif
+// Wait states the asm relies on (gfx950, MI355X_MICROARCH / the ISA's MFMA hazard table): a
+// VALU write of an MFMA's srcA/B/C needs 2 before the MFMA (the `s_nop 1` in front of each
+// asm MFMA; it issues while the previous MFMA holds the pipe); an f64 16x16x4 MFMA's result
+// read by VALU / VMEM / a non-dependent MFMA needs up to 18 (gram_asm_drain's 3 × s_nop 7 at the
+// loop exit).  tests/test_isa.py checks the compiled Gram loop: MFMAs only on pinned tiles,
+// no v_accvgpr moves or scratch between them.
 #ifndef QMFX_F64_AG
 #define QMFX_F64_AG 24
 #endif
@@ -254,8 +260,10 @@ __device__ __forceinline__ void gram_step_pinned(f64x4 (&acc)[NTT], const double
 // chunk's (column, value) pairs are loaded a whole chunk ahead.
 template <typename T, int NT>
 constexpr int plain_depth() {
-  // (fp64 k > 64 keeps its own one-step loop: gram_plain's ring spills 546 VGPRs there even
-  // with VGPR-form accumulators)
+  // fp64 k = 80..128 row and heavy-row solves: a ring of QMFX_F64_PD = 2 (the pinned
+  // accumulators leave room for two row buffers: round 5, profiles/r05/ab_f64_pinned_gram_c3.txt,
+  // 189.0 -> 180.0 ms per C3 item half); the one-step loop below remains only for the split-K
+  // segment instance (MODE 1)
   return (sizeof(T) == 8 && NT > 4) ? QMFX_F64_PD : 4;
 }
 template <int J>
@@ -508,8 +516,8 @@ void wals_direct_kernel(SolveArgs<T> a) {
     if constexpr (Perm<NT>::template split<T>) {
       gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
     } else if constexpr (sizeof(T) == 8 && NT > 4 && (!QMFX_F64_PLAIN || MODE == 1)) {
-      // fp64 k > 64 (one wave, accumulators across the whole register file): the ring of
-      // gram_plain costs more spills than its deeper prefetch gains; one step ahead
+      // fp64 k > 64, split-K segment Grams (MODE 1; QMFX_F64_PLAIN = 0 variants also): the
+      // one-step loop, one step ahead (the row solves take gram_plain's ring above);
       // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
       // so they contribute exactly nothing without per-value selects (only Σc needs the
       // validity)

@@ -301,7 +301,9 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 // YᵀY on the tiled multi-wave kernel (fp32 k > 128, fp64 k > 64)
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
 // direct rows on the multi-wave row kernel: k > 128 (fp64 k = 80..128 runs the one-wave
-// direct kernel with its accumulators across the VGPR + AGPR file)
+// direct kernel with its accumulators across the VGPR + AGPR file; the
+// multi-wave kernel at fp64 k = 128, four waves per row and two rows per CU, measured 213.7
+// against 179.2 ms per C3 item half in round 6)
 bool use_big_rows(const qmfx_ctx* c) { return c->nt > 8; }
 
 // Largest whitened-row bucket (NTN: n ≤ 16·NTN) for this factor tiling: n ≤ KP/2
@@ -821,6 +823,12 @@ int qmfx_import_signals(qmfx_ctx* dst, qmfx_ctx* src) {
     if (!s.rowptr || !s.col || s.h_rowptr.empty()) return fail("qmfx_import_signals: the source has no CSR");
     if (s.sharded) return fail("qmfx_import_signals: the source CSR is sharded");
   }
+  // the destination takes a whole CSR: one already partitioned into ranks would be overwritten
+  if (dst->comm || dst->world > 1 || dst->s[0].sharded || dst->s[1].sharded)
+    return fail("qmfx_import_signals: the destination already went through qmfx_dist_init");
+  // the source's CSR writes (its own stream) complete before the copies on dst's stream
+  if (set_dev(src)) return -2;
+  HIPCHK(hipStreamSynchronize(src->stream));
   if (int rc = qmfx_set_shape(dst, src->s[0].n, src->s[1].n)) return rc;
   if (set_dev(dst)) return -2;
   for (int side = 0; side < 2; ++side) {

@@ -72,6 +72,11 @@ struct BigCfg {
   // one wave-specialised copy of the row solve per wave (compile-time tile map) and the LDLᵀ
   // factorization (big_ldl_solve): the streamed fp64 rows and the split fp32 rows
   static constexpr bool WSPEC = STREAM || (SPLIT && QMFX_BIG_LDL32);
+  // waves per SIMD the row kernel is compiled for (512-thread workgroups: two)
+  static constexpr int WPE = (64 * NW + 255) / 256;
+  // LDLᵀ panel buffers: two (no barrier between a panel's readers and the next panel's
+  // stores), or one when more than two workgroups share a CU's LDS
+  static constexpr bool PANEL2 = WSPEC && (NT > 8 || WPE <= 2);
   static constexpr int TPW = PAIR ? NT + 1 : (NTT + NW - 1) / NW;
   static constexpr int SPAD = 40;  // bf16 per plane column (32 signals + 16 B pad: no bank conflicts)
   static constexpr int NTHR = 64 * NW;
@@ -122,7 +127,7 @@ struct BigShared {
     struct {
       T panel[C::KP * C::PLD];
       T Ldiag[NT * 16 * C::PLD];
-      T panel2[C::WSPEC ? C::KP * C::PLD : 1];  // LDLᵀ factorization: odd panels
+      T panel2[C::PANEL2 ? C::KP * C::PLD : 1];  // LDLᵀ factorization: odd panels
     };
   };
   T w[2][C::SIG];   // α·v of the staged signals (0 past the row end)
@@ -518,7 +523,7 @@ __device__ __forceinline__ void big_ldl_solve(BigShared<T, NT>& S,
   auto stamp = [&]() -> uint64_t { return sub ? __builtin_amdgcn_s_memtime() : 0; };
   t0 = stamp();
   for (int p = 0; p < NT; ++p) {
-    T* P = (p & 1) ? S.panel2 : S.panel;
+    T* P = (C::PANEL2 && (p & 1)) ? S.panel2 : S.panel;
     const int R = KP - 16 * p;
     // (a)
 #pragma unroll
@@ -616,6 +621,8 @@ __device__ __forceinline__ void big_ldl_solve(BigShared<T, NT>& S,
         }
       }
     }
+    // one panel buffer: its readers finish before the next panel's stores
+    if constexpr (!C::PANEL2) __syncthreads();
     if (sub) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const uint64_t t = stamp();
@@ -1123,7 +1130,7 @@ __device__ __forceinline__ void big_row_body(const SolveArgs<T>& a, BigShared<T,
 }
 
 template <typename T, int NT, int MODE = 0>
-__global__ __launch_bounds__((BigCfg<T, NT>::NTHR)) void wals_big_kernel(SolveArgs<T> a) {
+__global__ __launch_bounds__((BigCfg<T, NT>::NTHR), (BigCfg<T, NT>::WPE)) void wals_big_kernel(SolveArgs<T> a) {
   using C = BigCfg<T, NT>;
   __shared__ __attribute__((aligned(16))) BigShared<T, NT> S;
   if constexpr (C::WSPEC) {

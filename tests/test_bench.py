@@ -95,7 +95,9 @@ def _exchange_rank(rank, world, port, q):
         t = torch.tensor(vals, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return [float(v) for v in t]
-    q.put((rank, bench.exchange_fields(stats, 2, reduce_max)))
+    model = {0: bench.exchange_model(10_000_000, 128, 8, world),
+             1: bench.exchange_model(1_000_000, 128, 8, world)}
+    q.put((rank, bench.exchange_fields(stats, 2, reduce_max, model)))
     dist.destroy_process_group()
 
 
@@ -119,8 +121,16 @@ def test_exchange_fields_are_max_over_ranks_gloo_world2():
     assert res[0] == res[1]
     f = res[0]
     assert set(f) == {"user_half", "item_half"}
-    assert f["user_half"] == {"exchange_ms": 11.0, "exposed_ms": 2.0, "solve_ms": 20.0}
-    assert f["item_half"] == {"exchange_ms": 12.0, "exposed_ms": 2.0, "solve_ms": 20.0}
+    keys = ("exchange_ms", "exposed_ms", "solve_ms")
+    assert {k: f["user_half"][k] for k in keys} == {"exchange_ms": 11.0, "exposed_ms": 2.0,
+                                                    "solve_ms": 20.0}
+    assert {k: f["item_half"][k] for k in keys} == {"exchange_ms": 12.0, "exposed_ms": 2.0,
+                                                    "solve_ms": 20.0}
+    # the DESIGN §6 model beside the measurement: C3 fp64 user half, world 2: half of 10.24 GB
+    p = f["user_half"]["predicted"]
+    assert p["bytes_in_per_rank"] == 10_000_000 * 128 * 8 / 2
+    assert abs(p["model_ms_bus"] - 5.12e9 / 350e9 * 1e3) < 1e-3
+    assert f["user_half"]["measured_gbs_in_per_rank"] == round(5.12e9 / 11.0 / 1e6, 1)
 
 
 def _fake_stats(d_ms, w_ms, d_side_ms, w_side_ms):

@@ -22,12 +22,13 @@ c.wals_half(side, 40.0, 0.05)
 c.wals_half(side, 40.0, 0.05)
 t = np.fromfile(path + "_side%d.bin" % side, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
 os.remove(path + "_side%d.bin" % side)
-# rows without a record (all-zero: the split-K heavy rows' segment/solve launches do not
-# stamp) are left out, and counted so their absence is visible
+# rows without a record (all-zero: the split-K heavy rows' segment/solve launches and the fp32
+# streamed whitened kernel, which has no traced instance, do not stamp) are left out, and
+# counted so their absence is visible
 untraced = int((t[:, 0] == 0).sum())
 t = t[t[:, 0] > 0]
 if untraced:
-    print("rows without a trace record (split-K heavy rows), left out:", untraced)
+    print("rows without a trace record (split-K heavy rows; fp32 whitened rows), left out:", untraced)
 ph = np.diff(t[:, 0:5], axis=1)  # load, K+setup, chol, x'+store
 n = t[:, 6]
 print("rows traced", len(t))
