@@ -302,8 +302,8 @@ hipError_t scopy(qmfx_ctx* c, void* dst, const void* src, size_t bytes, hipMemcp
 bool use_big(const qmfx_ctx* c) { return c->prec == 32 ? c->nt > 8 : c->nt > 4; }
 // direct rows on the multi-wave row kernel: k > 128 (fp64 k = 80..128 runs the one-wave
 // direct kernel with its accumulators across the VGPR + AGPR file; the
-// multi-wave kernel at fp64 k = 128, four waves per row and two rows per CU, measured 213.7
-// against 179.2 ms per C3 item half in round 6)
+// multi-wave kernel at fp64 k = 128 measured 213.7 ms per C3 item half at four waves per row
+// and 206.5 ms at two, against 179.2 / 175.6 ms here: round 6, profiles/r06/ab_big128_c3_f64.txt)
 bool use_big_rows(const qmfx_ctx* c) { return c->nt > 8; }
 
 // Largest whitened-row bucket (NTN: n ≤ 16·NTN) for this factor tiling: n ≤ KP/2

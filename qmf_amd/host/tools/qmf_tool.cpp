@@ -68,9 +68,9 @@ static int genDataset(long long nu, long long ni, long long nnz, unsigned long l
         const unsigned long long key =
             (unsigned long long)(((unsigned __int128)a * (unsigned long long)j + b) % space);
         char* p = buf;
-        p = std::to_chars(p, buf + 64, (long long)(key / ni)).ptr;
+        p = std::to_chars(p, buf + 24, (long long)(key / ni)).ptr;  // ≤ 20 digits each
         *p++ = ' ';
-        p = std::to_chars(p, buf + 64, (long long)(key % ni)).ptr;
+        p = std::to_chars(p, p + 24, (long long)(key % ni)).ptr;
         *p++ = ' ';
         *p++ = (char)('1' + mix64(seed ^ (unsigned long long)j) % 5);
         *p++ = '\n';
