@@ -543,8 +543,9 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
           for (int I = 0; I < NTN; ++I) v += cur[I][h][c] * ul[I];
           sx[h][c] = v;
         }
-      row16_sum4(sx[0]);
-      row16_sum4(sx[1]);
+      // column 32s + 8kk + row16_sum8_column(cl) of x' in the lanes with cl & 2 == 0 (and
+      // their neighbours)
+      const float sxc = row16_sum8_split(sx, cl);
       if (hasQ) {
         float sb[2][4];
 #pragma unroll
@@ -556,23 +557,14 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
             for (int I = 0; I < NTN; ++I) v += cur[I][h][c] * cv[I];
             sb[h][c] = v;
           }
-        row16_sum4(sb[0]);
-        row16_sum4(sb[1]);
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) xbq += (double)sx[h][c] * (double)sb[h][c];
+        const float sbc = row16_sum8_split(sb, cl);
+        xbq += (cl & 2) == 0 ? (double)sxc * (double)sbc : 0.0;
       }
-      // lanes cl = 0, 1 of each 16-lane row store columns 32s + 8kk + 4cl .. +3
-      if (cl < 2 && 32 * s + 8 * kk < KP) {
-        f32x4 o = cl == 0 ? f32x4{sx[0][0], sx[0][1], sx[0][2], sx[0][3]}
-                          : f32x4{sx[1][0], sx[1][1], sx[1][2], sx[1][3]};
-        if (bad) o = f32x4{0.f, 0.f, 0.f, 0.f};
-        reinterpret_cast<f32x4*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
-      }
+      if ((cl & 2) == 0 && 32 * s + 8 * kk < KP)
+        a.X[row * KP + 32 * s + 8 * kk + row16_sum8_column(cl)] = bad ? 0.f : sxc;
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
+    if (hasQ) xb = wave_sum(xbq);
   }
   double cs = 0.0;
 #pragma unroll
@@ -907,7 +899,8 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
         for (int I = 0; I < NTN; ++I) v += cur[I][c] * ul[I];
         sx[c] = v;
       }
-      row16_sum4(sx);
+      // column 16s + 4kk + (cl >> 2) of x' in lanes cl = 0, 4, 8, 12 (and their neighbours)
+      const double sxc = row16_sum4_split(sx, cl);
       if (hasQ) {
         double sb[4];
 #pragma unroll
@@ -917,16 +910,10 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
           for (int I = 0; I < NTN; ++I) v += cur[I][c] * cv[I];
           sb[c] = v;
         }
-        row16_sum4(sb);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) xbq += sx[c] * sb[c];
+        const double sbc = row16_sum4_split(sb, cl);
+        xbq += (cl & 3) == 0 ? sxc * sbc : 0.0;
       }
-      // lanes cl = 0, 1 of each 16-lane row store columns 16s + 4kk + 2cl .. +1
-      if (cl < 2) {
-        f64x2 o = cl == 0 ? f64x2{sx[0], sx[1]} : f64x2{sx[2], sx[3]};
-        if (bad) o = f64x2{0.0, 0.0};
-        reinterpret_cast<f64x2*>(a.X + row * KP)[8 * s + 2 * kk + cl] = o;
-      }
+      if ((cl & 3) == 0) a.X[row * KP + 16 * s + 4 * kk + (cl >> 2)] = bad ? 0.0 : sxc;
       __builtin_amdgcn_sched_barrier(0);
     };
     // the kept chunks while the first gathers are in flight, then the gathered ring
@@ -946,7 +933,7 @@ __global__ __launch_bounds__(64, wb64_waves<NTN>()) void wals_woodbury_st64_kern
       if (q + XD < NG) load_chunk_x(KT + q + XD, buf[(q + XD) % (XD + 1)]);
       xchunk(KT + q, buf[q % (XD + 1)]);
     }
-    if (hasQ) xb = wave_sum(cl == 0 ? xbq : 0.0);
+    if (hasQ) xb = wave_sum(xbq);
   }
   double cs = 0.0;
 #pragma unroll
