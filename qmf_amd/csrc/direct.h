@@ -268,7 +268,9 @@ constexpr int plain_depth() {
 }
 template <int J>
 __device__ __forceinline__ int row_bcast(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, false);
+  // every lane has a source lane: no old operand (update_dpp(0, …) zero-initialised the
+  // destination with one more v_mov per broadcast)
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, true);
 }
 template <int J>
 __device__ __forceinline__ float row_bcast(float v) {

@@ -463,7 +463,7 @@ __device__ __forceinline__ void split3x4(const float (&x)[4], uint2& h, uint2& m
 // fp32 twin of chol.h's bcast16 (lane J of every 16-lane row)
 template <int J>
 __device__ __forceinline__ float bcast16(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xf, 0xf, true));
 }
 // Column C of a panel in the replicated-diagonal layout (chol.h dg_column, for either precision):
 // the pivot d = U[C][C] and z_C = b_C broadcast from lane C of every 16-lane row, the
