@@ -1050,6 +1050,133 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
   }
 }
 
+// The same GEMMs for KP ≤ 128 with L⁻¹ staged once per workgroup in LDS (round 6).  The
+// global-operand kernel above keeps its L⁻¹ fragments in the same VMEM queue as the row
+// gathers: of the ~18 loads a wave has in flight, two in seven are row bytes, so the rows
+// (the kernel's HBM traffic) arrive at ~3 TB/s (C3 fp64 unwhiten: 21.6 GB in 6.7 ms, PMC).
+// Here the B operand is an LDS read, every VMEM load in flight is a row load, and the grid
+// is persistent (one or two 512-thread workgroups per CU, each wave striding over 32-row
+// blocks), so L⁻¹ crosses the fabric once per workgroup instead of once per 32 rows.
+//   LDS layout: B[m][j] (= Linv[m][j] to unwhiten, Linv[j][m] to whiten) with a row pitch of
+//   KP + 128 B, so the four K rows of one fragment read (lanes kk = 0..3) fall on two
+//   disjoint halves of the banks.
+// ---------------------------------------------------------------------------------------
+#ifndef QMFX_WHITEN_LDS
+#define QMFX_WHITEN_LDS 1
+#endif
+#ifndef QMFX_WHITEN_LDS_D
+#define QMFX_WHITEN_LDS_D 4
+#endif
+template <typename T, int NT>
+struct WhitenLds {
+  static constexpr int KP = 16 * NT;
+  static constexpr int LDL = KP + 128 / (int)sizeof(T);
+  static constexpr int BYTES = KP * LDL * (int)sizeof(T);
+  // fp64 only: at fp32 (C3) the global-operand kernel measured equal or faster
+  // (profiles/r06/ab_whiten_lds.txt)
+  static constexpr bool FITS = sizeof(T) == 8 && NT <= 8 && BYTES <= 150 * 1024;
+  // workgroups per CU the LDS allows (at most 2: 16 waves)
+  static constexpr int PER_CU = BYTES <= 75 * 1024 ? 2 : 1;
+};
+template <typename T, int NT, bool UNWHITEN>
+__global__ __launch_bounds__(512) void whiten_lds_kernel(const T* in, T* out,
+                                                         const int64_t* order, int64_t nrows,
+                                                         const T* __restrict__ Linv,
+                                                         double* rowloss, double lambda) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  using W = WhitenLds<T, NT>;
+  constexpr int KP = W::KP;
+  constexpr int LDL = W::LDL;
+  constexpr int RG = QMFX_WHITEN_RG;
+  __shared__ __attribute__((aligned(16))) T B[KP * LDL];
+  for (int i = threadIdx.x; i < KP * KP; i += 512) {
+    const int r = i / KP, c = i % KP;
+    const T v = Linv[i];
+    if (UNWHITEN)
+      B[r * LDL + c] = v;
+    else
+      B[c * LDL + r] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int cl = lane & 15;
+  const int kk = lane >> 4;
+  const int64_t stride = (int64_t)gridDim.x * 8 * (16 * RG);
+  for (int64_t rw = ((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * (16 * RG); rw < nrows;
+       rw += stride) {
+    int64_t rowa[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const int64_t r = rw + 16 * g + cl;
+      const int64_t ra = r < nrows ? r : nrows - 1;
+      rowa[g] = UNWHITEN ? order[ra] : ra;
+    }
+    acc_t acc[RG][NT];
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+      for (int J = 0; J < NT; ++J) acc[g][J] = acc_t{0, 0, 0, 0};
+    // the row values of step s + D are in flight while step s's MFMAs run (each step is its
+    // own scheduling region, or the compiler hoists every step's LDS reads and spills)
+    constexpr int NS = KP / 4;
+    constexpr int D = QMFX_WHITEN_LDS_D < NS ? QMFX_WHITEN_LDS_D : NS;
+    T ring[D][RG];
+#pragma unroll
+    for (int s = 0; s < D; ++s)
+#pragma unroll
+      for (int g = 0; g < RG; ++g) ring[s][g] = in[rowa[g] * KP + 4 * s + kk];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int m = 4 * s + kk;
+      T av[RG];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) av[g] = ring[s % D][g];
+      if (s + D < NS) {
+#pragma unroll
+        for (int g = 0; g < RG; ++g) ring[s % D][g] = in[rowa[g] * KP + 4 * (s + D) + kk];
+      }
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+        // unwhiten: x_j = Σ_{m ≥ j} Linv[m][j] x'_m; whiten: z_j = Σ_{m ≤ j} Linv[j][m] y_m
+        const bool live = UNWHITEN ? (4 * s + 3 >= 16 * J) : (4 * s <= 16 * J + 15);
+        if (live) {
+          const T bv = B[m * LDL + 16 * J + cl];
+#pragma unroll
+          for (int g = 0; g < RG; ++g) acc[g][J] = M::mma(av[g], bv, acc[g][J]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // all reads of this block's rows are done before any write (in-place unwhitening)
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const int64_t r0 = rw + 16 * g;
+      T ss[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t ro = r0 + M::crow(lane, r);
+        if (ro < nrows) {
+          const int64_t rowo = UNWHITEN ? order[ro] : ro;
+#pragma unroll
+          for (int J = 0; J < NT; ++J) {
+            out[rowo * KP + 16 * J + cl] = acc[g][J][r];
+            ss[r] += acc[g][J][r] * acc[g][J][r];
+          }
+        }
+      }
+      if (UNWHITEN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const T tot = row16_sum(ss[r]);
+          const int64_t ro = r0 + M::crow(lane, r);
+          if (cl == 0 && ro < nrows) rowloss[order[ro]] -= lambda * (double)tot;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // M = G + λI (padding: 1) → L (Cholesky, fp64, in LDS) → Linv = L⁻¹ written in T.
 // One 256-thread workgroup; run once per half when whitened rows exist.
@@ -1212,6 +1339,24 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
                                    const T* Linv, double* rowloss, double lambda, bool unwhiten,
                                    hipStream_t s) {
   if (nrows <= 0) return hipSuccess;
+#if QMFX_WHITEN_LDS
+  if constexpr (WhitenLds<T, NT>::FITS) {
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const int64_t need = (nrows + 8 * 16 * QMFX_WHITEN_RG - 1) / (8 * 16 * QMFX_WHITEN_RG);
+    const int64_t cap = (int64_t)cus * WhitenLds<T, NT>::PER_CU;
+    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    if (unwhiten)
+      hipLaunchKernelGGL((whiten_lds_kernel<T, NT, true>), dim3(grid), dim3(512), 0, s, in, out,
+                         order, nrows, Linv, rowloss, lambda);
+    else
+      hipLaunchKernelGGL((whiten_lds_kernel<T, NT, false>), dim3(grid), dim3(512), 0, s, in,
+                         out, order, nrows, Linv, rowloss, lambda);
+    return hipGetLastError();
+  }
+#endif
   const unsigned blocks = (unsigned)((nrows + 64 * QMFX_WHITEN_RG - 1) / (64 * QMFX_WHITEN_RG));
   if (unwhiten)
     hipLaunchKernelGGL((whiten_kernel<T, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, order,
