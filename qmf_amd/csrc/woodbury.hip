@@ -1346,7 +1346,13 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     const int64_t need = (nrows + 8 * 16 * QMFX_WHITEN_RG - 1) / (8 * 16 * QMFX_WHITEN_RG);
-    const int64_t cap = (int64_t)cus * WhitenLds<T, NT>::PER_CU;
+    int64_t cap = (int64_t)cus * WhitenLds<T, NT>::PER_CU;
+    // test hook (read per launch): fewer workgroups, so that every wave strides over several
+    // 32-row blocks at test sizes
+    if (const char* g = std::getenv("QMFX_WHITEN_GRID")) {
+      const long v = std::strtol(g, nullptr, 10);
+      if (v > 0 && v < cap) cap = v;
+    }
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     if (unwhiten)
       hipLaunchKernelGGL((whiten_lds_kernel<T, NT, true>), dim3(grid), dim3(512), 0, s, in, out,

@@ -344,10 +344,36 @@ def test_row_chunked_launches_bit_identical(k, monkeypatch):
     chunks (QMFX_ROW_CHUNK) must not change a single bit."""
     u, i, v = synth(1200, 300, 30000, seed=9)
     _, c1 = make_pair(u, i, v, k, 32, seed=6)
-    monkeypatch.setenv("QMFX_ROW_CHUNK", "37")
     _, c2 = make_pair(u, i, v, k, 32, seed=6)
     for side in (0, 1):
         l1 = c1.wals_half(side, ALPHA, LAM)
+        # the chunk is read per launch: set only around the chunked context's half
+        monkeypatch.setenv("QMFX_ROW_CHUNK", "37")
         l2 = c2.wals_half(side, ALPHA, LAM)
+        monkeypatch.delenv("QMFX_ROW_CHUNK")
         assert np.array_equal(c1.factors(side), c2.factors(side)), side
         assert l1 == l2, side
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_whitening_grid_strides_bit_identical(k, monkeypatch):
+    """fp64 k ≤ 128 whitening GEMMs (x = L⁻ᵀx' over the whitened rows, Z = YL⁻ᵀ over the
+    fixed side) run on a persistent grid with L⁻¹ in LDS (whiten_lds_kernel).  Cut to one
+    workgroup (QMFX_WHITEN_GRID=1, read per launch) every wave strides over ~80 32-row
+    blocks; the half must not change a bit, and it must match the oracle."""
+    u, i, v = synth(20000, 900, 300000, seed=13)  # ~15 signals per user: users whitened
+    o, c1 = make_pair(u, i, v, k, 64, seed=2)
+    _, c2 = make_pair(u, i, v, k, 64, seed=2)
+    assert sum(c1.row_classes(0)["whitened"]) > 15000
+    for side in (0, 1):
+        lo = o.iterate(side, NTHR)
+        l1 = c1.wals_half(side, ALPHA, LAM)
+        monkeypatch.setenv("QMFX_WHITEN_GRID", "1")
+        l2 = c2.wals_half(side, ALPHA, LAM)
+        monkeypatch.delenv("QMFX_WHITEN_GRID")
+        assert np.array_equal(c1.factors(side), c2.factors(side)), side
+        assert l1 == l2, side
+        assert rel_err(c1.factors(side), o.factors(side)) < 1e-9, side
+        assert abs(l1 / (o.nusers * o.nitems) - lo) < 1e-9 * abs(lo), side
+        c1.set_factors(side, o.factors(side))
+        c2.set_factors(side, o.factors(side))
