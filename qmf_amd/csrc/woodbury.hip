@@ -591,8 +591,10 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 #ifndef QMFX_WB64_KD
 #define QMFX_WB64_KD 1
 #endif
+// (x' pass: 2 since round 6, −0.9 ms per C3 fp64 user half same box, profiles/r06/
+// ab_whiten_lds.txt; round 3 had measured no gain with more chunks kept on chip)
 #ifndef QMFX_WB64_XD
-#define QMFX_WB64_XD 1
+#define QMFX_WB64_XD 2
 #endif
 #ifndef QMFX_WB64_LTP
 #define QMFX_WB64_LTP 1
@@ -1067,14 +1069,21 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
 #ifndef QMFX_WHITEN_LDS_D
 #define QMFX_WHITEN_LDS_D 4
 #endif
+#ifndef QMFX_WHITEN_LDS32
+#define QMFX_WHITEN_LDS32 0
+#endif
 template <typename T, int NT>
 struct WhitenLds {
   static constexpr int KP = 16 * NT;
-  static constexpr int LDL = KP + 128 / (int)sizeof(T);
+  // row pitch: fp64 KP + 128 B (a fragment read's four K rows of 128 B on two bank halves),
+  // fp32 KP + 64 B (four 64-B rows on four bank quarters; 72 KB at k = 128, two workgroups
+  // per CU)
+  static constexpr int LDL = KP + (sizeof(T) == 8 ? 16 : 16);
   static constexpr int BYTES = KP * LDL * (int)sizeof(T);
-  // fp64 only: at fp32 (C3) the global-operand kernel measured equal or faster
-  // (profiles/r06/ab_whiten_lds.txt)
-  static constexpr bool FITS = sizeof(T) == 8 && NT <= 8 && BYTES <= 150 * 1024;
+  // fp64 only by default: at fp32 (C3) the kernel measured slower with one workgroup per CU
+  // (profiles/r06/ab_whiten_lds.txt); QMFX_WHITEN_LDS32 = 1 enables the two-per-CU form
+  static constexpr bool FITS =
+      (sizeof(T) == 8 || QMFX_WHITEN_LDS32) && NT <= 8 && BYTES <= 150 * 1024;
   // workgroups per CU the LDS allows (at most 2: 16 waves)
   static constexpr int PER_CU = BYTES <= 75 * 1024 ? 2 : 1;
 };
