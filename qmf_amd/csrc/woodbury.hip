@@ -1072,6 +1072,9 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
 #ifndef QMFX_WHITEN_LDS32
 #define QMFX_WHITEN_LDS32 0
 #endif
+#ifndef QMFX_WHITEN_LDS_RG
+#define QMFX_WHITEN_LDS_RG 2
+#endif
 template <typename T, int NT>
 struct WhitenLds {
   static constexpr int KP = 16 * NT;
@@ -1097,7 +1100,7 @@ __global__ __launch_bounds__(512) void whiten_lds_kernel(const T* in, T* out,
   using W = WhitenLds<T, NT>;
   constexpr int KP = W::KP;
   constexpr int LDL = W::LDL;
-  constexpr int RG = QMFX_WHITEN_RG;
+  constexpr int RG = QMFX_WHITEN_LDS_RG;
   __shared__ __attribute__((aligned(16))) T B[KP * LDL];
   for (int i = threadIdx.x; i < KP * KP; i += 512) {
     const int r = i / KP, c = i % KP;
@@ -1354,7 +1357,7 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    const int64_t need = (nrows + 8 * 16 * QMFX_WHITEN_RG - 1) / (8 * 16 * QMFX_WHITEN_RG);
+    const int64_t need = (nrows + 8 * 16 * QMFX_WHITEN_LDS_RG - 1) / (8 * 16 * QMFX_WHITEN_LDS_RG);
     int64_t cap = (int64_t)cus * WhitenLds<T, NT>::PER_CU;
     // test hook (read per launch): fewer workgroups, so that every wave strides over several
     // 32-row blocks at test sizes
