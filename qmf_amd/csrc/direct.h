@@ -211,6 +211,10 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_F64_PLAIN
 #define QMFX_F64_PLAIN 1
 #endif
+// the ring depth of the other gram_plain instances (fp32 k ≤ 80, fp64 k ≤ 64)
+#ifndef QMFX_PLAIN_PD
+#define QMFX_PLAIN_PD 4
+#endif
 #ifndef QMFX_F64_PD
 #define QMFX_F64_PD 2
 #endif
@@ -264,7 +268,7 @@ constexpr int plain_depth() {
   // accumulators leave room for two row buffers: round 5, profiles/r05/ab_f64_pinned_gram_c3.txt,
   // 189.0 -> 180.0 ms per C3 item half); the one-step loop below remains only for the split-K
   // segment instance (MODE 1)
-  return (sizeof(T) == 8 && NT > 4) ? QMFX_F64_PD : 4;
+  return (sizeof(T) == 8 && NT > 4) ? QMFX_F64_PD : QMFX_PLAIN_PD;
 }
 template <int J>
 __device__ __forceinline__ int row_bcast(int v) {
