@@ -1388,6 +1388,9 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
 // The same factorization for KP > 128 (the fp64 matrix exceeds LDS): one 1024-thread
 // workgroup on a global fp64 scratch of KP·(KP+1) doubles (L2-resident; __syncthreads
 // orders the block's global accesses).  Once per half; ≈ms at KP = 256.
+#ifndef QMFX_CHOL_INV4
+#define QMFX_CHOL_INV4 1
+#endif
 template <typename T, int NT>
 __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k, double lambda,
                                                                T* Linv, int32_t* status,
@@ -1421,6 +1424,26 @@ __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k
     }
     __syncthreads();
   }
+#if QMFX_CHOL_INV4
+  // L⁻¹ column c by forward substitution on four threads (lanes 4c .. 4c + 3 of one wave):
+  // thread q sums the terms mm ≡ q (mod 4), two shuffles combine them, and entry i is stored
+  // by the thread that will read it again (q = i mod 4), so each thread only re-reads its own
+  // writes.  One thread per column left the k = 256 launch at 6.2 ms, the column chains
+  // (up to 32K dependent-address FMAs) being the whole of it.
+  {
+    const int c = tid >> 2, q = tid & 3;
+    if (c < KP) {
+      for (int i = c + 1; i < KP; ++i) {
+        double sm = q == 0 ? A[i * LD + c] * dinv[c] : 0.0;
+        int mm = c + 1 + ((q - (c + 1)) & 3);
+        for (; mm < i; mm += 4) sm += A[i * LD + mm] * A[c * LD + mm];
+        sm += __shfl_xor(sm, 1, 64);
+        sm += __shfl_xor(sm, 2, 64);
+        if ((i & 3) == q) A[c * LD + i] = -sm * dinv[i];
+      }
+    }
+  }
+#else
   if (tid < KP) {
     const int c = tid;
     for (int i = c + 1; i < KP; ++i) {
@@ -1429,6 +1452,7 @@ __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k
       A[c * LD + i] = -sm * dinv[i];
     }
   }
+#endif
   __syncthreads();
   for (int idx = tid; idx < KP * KP; idx += 1024) {
     const int i = idx / KP, c = idx % KP;
