@@ -1060,8 +1060,8 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
 // is persistent (one or two 512-thread workgroups per CU, each wave striding over 32-row
 // blocks), so L⁻¹ crosses the fabric once per workgroup instead of once per 32 rows.
 //   LDS layout: B[m][j] (= Linv[m][j] to unwhiten, Linv[j][m] to whiten) with a row pitch of
-//   KP + 128 B, so the four K rows of one fragment read (lanes kk = 0..3) fall on two
-//   disjoint halves of the banks.
+//   KP + 16 elements (fp64: + 128 B), so the four K rows of one fragment read (lanes kk =
+//   0..3) fall on two disjoint halves of the banks.
 // ---------------------------------------------------------------------------------------
 #ifndef QMFX_WHITEN_LDS
 #define QMFX_WHITEN_LDS 1
@@ -1078,10 +1078,10 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
 template <typename T, int NT>
 struct WhitenLds {
   static constexpr int KP = 16 * NT;
-  // row pitch: fp64 KP + 128 B (a fragment read's four K rows of 128 B on two bank halves),
-  // fp32 KP + 64 B (four 64-B rows on four bank quarters; 72 KB at k = 128, two workgroups
-  // per CU)
-  static constexpr int LDL = KP + (sizeof(T) == 8 ? 16 : 16);
+  // row pitch KP + 16 elements: fp64 KP + 128 B (a fragment read's four K rows of 128 B on
+  // two bank halves), fp32 KP + 64 B (four 64-B rows on four bank quarters; 72 KB at k = 128,
+  // two workgroups per CU)
+  static constexpr int LDL = KP + 16;
   static constexpr int BYTES = KP * LDL * (int)sizeof(T);
   // fp64 only by default: at fp32 (C3) the kernel measured slower with one workgroup per CU
   // (profiles/r06/ab_whiten_lds.txt); QMFX_WHITEN_LDS32 = 1 enables the two-per-CU form
