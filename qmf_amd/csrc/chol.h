@@ -72,9 +72,6 @@ __device__ __forceinline__ void lds_row_store(T* dst, const T (&v)[16]) {
   }
 }
 
-#ifndef QMFX_BW_DPP
-#define QMFX_BW_DPP 1
-#endif
 // LDS ordering inside chol_solve.  chol_solve REQUIRES a single-wave workgroup: LDS accesses
 // of one wave execute in order, so draining them and pinning the compiler's order is enough
 // (no s_barrier; the same speed as a plain compiler fence in the micro-benchmark,
@@ -202,8 +199,7 @@ __device__ __forceinline__ void slot_column(const double (&dg)[16], double invv,
 //   The trailing update A(I,J) −= U(I,p) D⁻¹ U(J,p)ᵀ is 4 MFMAs per tile with operands from
 //   the LDS panel (the J operand scaled by 1/d of its column); the diagonal blocks go to LDS
 //   transposed and scaled, Lt[q][c] = U[c][q]/d_q (c > q), for the backward substitution
-//   (QMFX_BW_DPP, the default: one v_fmac_dpp row_newbcast per column instead of a readlane
-//   + an FMA).
+//   (one v_fmac_dpp row_newbcast per column instead of a readlane + an FMA).
 // In: acc = lower 16×16 tiles of the SPD matrix; S.bw = right-hand side.  Out: S.xs = x.
 // `bad` is set on a pivot that is not positive (or not finite).
 // ---------------------------------------------------------------------------------------
@@ -350,11 +346,7 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     for (int it = 0; it < 4; ++it) {
       const int idx = lane + 64 * it;
       const int r = idx >> 4, c = idx & 15;
-#if QMFX_BW_DPP
       ltv[it] = c < r ? -(S.panel[r * PLD + c] * S.invd[16 * p + c]) : T(0);
-#else
-      ltv[it] = c < r ? S.panel[r * PLD + c] * S.invd[16 * p + c] : T(0);
-#endif
     }
     if constexpr (!LTP) {
 #pragma unroll
@@ -422,7 +414,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     T vm = (S.bw[16 * I + cl] - part) * S.invd[16 * I + cl];
     T lt[16];
     lds_row_load(S.lt_row(16 * I + cl), lt);
-#if QMFX_BW_DPP
     // x_c is lane c's vm in every 16-lane row: one DPP FMA per column (Lt stored negated),
     // padded for the next column's DPP read of the register it writes
     // (vm was just written by the compiler's VALU, which does not see this asm's DPP read:
@@ -431,10 +422,6 @@ __device__ __forceinline__ void chol_solve(typename Mfma<T>::acc_t (&acc)[NT * (
     [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
       (fmac_bcast16<15 - Cs, 1>(vm, vm, lt[15 - Cs]), ...);
     }(std::make_integer_sequence<int, 16>{});
-#else
-#pragma unroll
-    for (int c = 15; c >= 0; --c) vm -= lt[c] * readlane(vm, c);
-#endif
     if (lane < 16) S.xs[16 * I + lane] = vm;
     csync<WS>();
   }

@@ -207,10 +207,7 @@ __device__ __forceinline__ void gram_split_bf16(const SolveArgs<float>& a, int64
 #ifndef QMFX_F64_AG
 #define QMFX_F64_AG 24
 #endif
-// fp64 k > 64 on gram_plain (DPP-broadcast signal pairs, a ring of PD row buffers)
-#ifndef QMFX_F64_PLAIN
-#define QMFX_F64_PLAIN 1
-#endif
+// fp64 k > 64 row solves run gram_plain (DPP-broadcast signal pairs, a ring of PD row buffers)
 // the ring depth of the other gram_plain instances (fp32 k ≤ 80, fp64 k ≤ 64)
 #ifndef QMFX_PLAIN_PD
 #define QMFX_PLAIN_PD 4
@@ -521,8 +518,8 @@ void wals_direct_kernel(SolveArgs<T> a) {
     }
     if constexpr (Perm<NT>::template split<T>) {
       gram_split_bf16<NT>(a, beg, end, acc, bpart, csum, negw, lane, mcol, mval);
-    } else if constexpr (sizeof(T) == 8 && NT > 4 && (!QMFX_F64_PLAIN || MODE == 1)) {
-      // fp64 k > 64, split-K segment Grams (MODE 1; QMFX_F64_PLAIN = 0 variants also): the
+    } else if constexpr (sizeof(T) == 8 && NT > 4 && MODE == 1) {
+      // fp64 k > 64, split-K segment Grams (MODE 1): the
       // one-step loop, one step ahead (the row solves take gram_plain's ring above);
       // signals past the row's end gather the fixed side's all-zero row a.zrow with v = 0,
       // so they contribute exactly nothing without per-value selects (only Σc needs the

@@ -29,11 +29,7 @@ __device__ __forceinline__ void pivot_sqrt(float d, float& l, float& inv) {
 // of 1/√d) instead of the correctly rounded √d and division (≈25 dependent fp64 operations
 // on the column loop's critical path: ≈30% of the k = 128 Cholesky).  A non-positive or
 // NaN pivot still yields NaN or ∞, which the callers' (0, ∞) test flags.
-#ifndef QMFX_F64_RSQ_NR
-#define QMFX_F64_RSQ_NR 1
-#endif
 __device__ __forceinline__ void pivot_sqrt(double d, double& l, double& inv) {
-#if QMFX_F64_RSQ_NR
   const double y = __builtin_amdgcn_rsq(d);
   double g = d * y, h = 0.5 * y;
   double r = __builtin_fma(-g, h, 0.5);
@@ -43,10 +39,6 @@ __device__ __forceinline__ void pivot_sqrt(double d, double& l, double& inv) {
   h = __builtin_fma(h, r, h);
   l = __builtin_fma(g, r, g);
   inv = 2.0 * h;
-#else
-  l = sqrt(d);
-  inv = 1.0 / l;
-#endif
 }
 
 // Sum over the 16 lanes of a DPP row (lanes 16g..16g+15); every lane receives the sum.

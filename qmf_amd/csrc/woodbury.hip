@@ -269,10 +269,8 @@ void wals_woodbury_kernel(SolveArgs<T> a) {
 #ifndef QMFX_WB_ST_WAVES
 #define QMFX_WB_ST_WAVES 3
 #endif
-// K on the bf16 matrix cores from split3 parts (1) or on the f32 matrix path (0)
-#ifndef QMFX_WBS_SPLIT
-#define QMFX_WBS_SPLIT 1
-#endif
+// K on the bf16 matrix cores from split3 parts (the exact f32 MFMA path measured slower at
+// k = 64 and 128: profiles/r06/ab_c2_f32_kpass.txt)
 // n×n buckets beyond 64 signals (NTN = 5..8, k = 256): each lane carries H = 2 signals (e
 // = lane and lane + 64); the registers of the wider tiles leave two or one waves per SIMD.
 template <int NTN>
@@ -371,7 +369,6 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
     for (int s = 0; s < NS; ++s) {
       if (s + KD < NS) load_chunk(s + KD, buf[(s + KD) % (KD + 1)]);
       f32x4 (&cur)[NTN][2] = buf[s % (KD + 1)];
-#if QMFX_WBS_SPLIT
       Split3 sp[NTN];
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
@@ -383,7 +380,6 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
         }
         split3(x, sp[I]);
       }
-#endif
       if (hasQ) {
         float g[2][4];
 #pragma unroll
@@ -405,7 +401,6 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
 #pragma unroll
             for (int c = 0; c < 4; ++c) sq[I] += cur[I][h][c] * g[h][c];
       }
-#if QMFX_WBS_SPLIT
 #pragma unroll
       for (int I = 0; I < NTN; ++I) {
 #pragma unroll
@@ -414,21 +409,6 @@ __global__ __launch_bounds__(64, wb_st_waves<NTN>()) void wals_woodbury_st_kerne
           acc[t] = mma_split6(sp[I], sp[J], acc[t]);
         }
       }
-#else
-      // exact fp32 products on the f32 matrix path: the j-th of a lane's 8 columns is
-      // the K index of MFMA j (K = the lane group's column 32s + 8g + j), no split VALU
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-#pragma unroll
-        for (int I = 0; I < NTN; ++I) {
-#pragma unroll
-          for (int J = 0; J <= I; ++J) {
-            const int t = tile_index(I, J);
-            acc[t] = M::mma(cur[I][j >> 2][j & 3], cur[J][j >> 2][j & 3], acc[t]);
-          }
-        }
-      }
-#endif
       // one chunk's splits and the next chunks' loads live at a time
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -623,9 +603,6 @@ constexpr int wb64_kdepth() {
 // re-gathered is 1/NTK of the second pass's bytes)
 // fp64 k = 64 whitened rows on the streamed kernel (round 5: C2 fp64 18.5 -> 17.6 ms/epoch
 // with n ≤ 48 whitened; the register-resident kernel measured slower there)
-#ifndef QMFX_WB64_K64
-#define QMFX_WB64_K64 1
-#endif
 #ifndef QMFX_WB64_KEEP2
 #define QMFX_WB64_KEEP2 6
 #endif
@@ -1063,9 +1040,6 @@ __global__ __launch_bounds__(256) void whiten_kernel(const T* in, T* out, const 
 //   KP + 16 elements (fp64: + 128 B), so the four K rows of one fragment read (lanes kk =
 //   0..3) fall on two disjoint halves of the banks.
 // ---------------------------------------------------------------------------------------
-#ifndef QMFX_WHITEN_LDS
-#define QMFX_WHITEN_LDS 1
-#endif
 #ifndef QMFX_WHITEN_LDS_D
 #define QMFX_WHITEN_LDS_D 4
 #endif
@@ -1351,7 +1325,6 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
                                    const T* Linv, double* rowloss, double lambda, bool unwhiten,
                                    hipStream_t s) {
   if (nrows <= 0) return hipSuccess;
-#if QMFX_WHITEN_LDS
   if constexpr (WhitenLds<T, NT>::FITS) {
     int dev = 0, cus = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1374,7 +1347,6 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
                          out, order, nrows, Linv, rowloss, lambda);
     return hipGetLastError();
   }
-#endif
   const unsigned blocks = (unsigned)((nrows + 64 * QMFX_WHITEN_RG - 1) / (64 * QMFX_WHITEN_RG));
   if (unwhiten)
     hipLaunchKernelGGL((whiten_kernel<T, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, order,
@@ -1388,9 +1360,6 @@ static hipError_t launch_whiten_nt(const T* in, T* out, const int64_t* order, in
 // The same factorization for KP > 128 (the fp64 matrix exceeds LDS): one 1024-thread
 // workgroup on a global fp64 scratch of KP·(KP+1) doubles (L2-resident; __syncthreads
 // orders the block's global accesses).  Once per half; ≈ms at KP = 256.
-#ifndef QMFX_CHOL_INV4
-#define QMFX_CHOL_INV4 1
-#endif
 template <typename T, int NT>
 __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k, double lambda,
                                                                T* Linv, int32_t* status,
@@ -1424,7 +1393,6 @@ __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k
     }
     __syncthreads();
   }
-#if QMFX_CHOL_INV4
   // L⁻¹ column c by forward substitution on four threads (lanes 4c .. 4c + 3 of one wave):
   // thread q sums the terms mm ≡ q (mod 4), two shuffles combine them, and entry i is stored
   // by the thread that will read it again (q = i mod 4), so each thread only re-reads its own
@@ -1443,16 +1411,6 @@ __global__ __launch_bounds__(1024) void chol_inv_global_kernel(const T* G, int k
       }
     }
   }
-#else
-  if (tid < KP) {
-    const int c = tid;
-    for (int i = c + 1; i < KP; ++i) {
-      double sm = A[i * LD + c] * dinv[c];
-      for (int mm = c + 1; mm < i; ++mm) sm += A[i * LD + mm] * A[c * LD + mm];
-      A[c * LD + i] = -sm * dinv[i];
-    }
-  }
-#endif
   __syncthreads();
   for (int idx = tid; idx < KP * KP; idx += 1024) {
     const int i = idx / KP, c = idx % KP;
@@ -1487,9 +1445,7 @@ hipError_t launch_wals_woodbury(const SolveArgs<float>& a, int nt, int ntn, hipS
 hipError_t launch_wals_woodbury(const SolveArgs<double>& a, int nt, int ntn, hipStream_t s) {
   // k = 64 .. 128 and 256 on the streamed fp64 kernel; the register-resident one below
   switch (nt) {
-#if QMFX_WB64_K64
     case 4: return launch_woodbury_st64_ntk<4>(a, ntn, s);
-#endif
     case 5: return launch_woodbury_st64_ntk<5>(a, ntn, s);
     case 6: return launch_woodbury_st64_ntk<6>(a, ntn, s);
     case 7: return launch_woodbury_st64_ntk<7>(a, ntn, s);
